@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Benchmark: global stiffness-matrix assembly of 3-D P2 linear elasticity (BASELINE.json metric
+"Melements/s assembled + achieved HBM GB/s, 3D P2 elasticity at 1/2/4/8 GPUs").
+
+One step = one fem.assemble_matrix(J, bcs) over the whole mesh — the reference's timed
+setJ region (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:849-860: zero + cell loop + scatter
++ bc diagonal), sparsity build excluded as in the reference. Inputs (mesh, dofmap, E, pattern)
+are resident in HBM before timing.
+
+Workload: config E's mesh — unit cube, 203^3 cubes x 6 Kuhn tetrahedra = 50,192,562 P2 cells,
+202,257,429 dofs — with the linear-elasticity J (d = 0), nu = 0.3, E = E_range[cell % 200]
+(libc srand(6575) table), x=0 clamped and x=1 prescribed. N > 1 ranks (one per GPU) shard the
+cube into z-slabs (strong scaling: fixed total mesh); shared slab-interface rows are summed with
+an RCCL exchange between slab neighbours (femasm.parallel).
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "fem-libraries_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+# algorithmic bytes per P2-tet cell under the element-stream model:
+# 4*nn (dofmap) + 4*nv (geometry dofmap) + 8*gdim*nv (coords) + 8*n_w (E) + 16*ndof^2
+B_E_P2_TET = 4 * 10 + 4 * 4 + 8 * 3 * 4 + 8 * 1 + 16 * 30 * 30  # = 14,560
+HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, Chip-level parameters)
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def build_problem(n, dev, z_range=None):
+    from femasm import fem, mesh
+
+    from femasm.materials import e_range
+
+    m = mesh.create_box((1.0, 1.0, 1.0), (n, n, n), mesh.CellType.tetrahedron, device=dev, z_range=z_range)
+    V = fem.functionspace(m, ("Lagrange", 2, (3,)))
+    ncell_global0 = (z_range[0] if z_range else 0) * n * n * 6
+    cid = torch.arange(m.num_cells, device=dev, dtype=torch.int64) + ncell_global0
+    E = torch.tensor(e_range(), dtype=torch.float64, device=dev)[cid % 200]
+    a = fem.form(fem.LinearElasticity(V, E=E, nu=0.3))
+    left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
+    right = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.ones_like(x[0])))
+    bcs = [fem.dirichletbc(0.0, left, V), fem.dirichletbc([0.01, 0.0, 0.0], right, V)]
+    return m, V, a, bcs
+
+
+def cpu_baseline(sample_n: int, reps: int):
+    """Oracle (C restatement of dolfinx assemble_cells + set_diagonal, 1 thread) on a bounded
+    P2-tet sample of the same workload; returns Melements/s."""
+    from femasm import fem, mesh
+    from femasm.materials import e_range
+    from oracle import oracle as O
+
+    m = mesh.create_unit_cube(sample_n, sample_n, sample_n, mesh.CellType.tetrahedron)
+    V = fem.functionspace(m, ("Lagrange", 2, (3,)))
+    cells = V.dofmap.numpy()
+    geom = m.cells.numpy()
+    x = m.x.numpy()
+    E = e_range()[np.arange(m.num_cells) % 200]
+    lam, mu = O.lame(E, 0.3)
+    left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
+    right = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.ones_like(x[0])))
+    bcs = [fem.dirichletbc(0.0, left, V), fem.dirichletbc([0.01, 0.0, 0.0], right, V)]
+    marker, _ = fem._combine_bcs(V, bcs)
+    bc = marker.numpy()
+    indptr, indices = O.sparsity(cells, V.num_nodes)
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        O.assemble_elasticity(-4, 2, cells, geom, x, lam, mu, indptr, indices, bc=bc, diag=1.0)  # zeroed inside
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return m.num_cells / t / 1e6, m.num_cells, t
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=203, help="cubes per side (config E: 203)")
+    ap.add_argument("--method", default="gather", choices=["gather", "scatter"])
+    ap.add_argument("--cpu-sample-n", type=int, default=24)
+    ap.add_argument("--cpu-reps", type=int, default=7)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+
+    from femasm import fem
+
+    n = args.n
+    t0 = time.time()
+    if world > 1:
+        from femasm import parallel
+
+        prob = parallel.SlabProblem(n, rank, world, dev)
+        step = prob.assemble
+        ncells_local = prob.num_cells
+        kernel_name = prob.kernel_name
+    else:
+        m, V, a, bcs = build_problem(n, dev)
+        A = fem.create_matrix(a)
+        fem.gather_plan(V, A)
+        ncells_local = m.num_cells
+
+        def step():
+            fem.assemble_matrix(a, bcs=bcs, A=A, method=args.method)
+
+    torch.cuda.synchronize()
+    log(f"[bench] setup {time.time() - t0:.1f}s: {ncells_local} cells on rank {rank}")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # per-launch kernel durations, HIP events on the launch stream (torch's current stream)
+    stream = torch.cuda.current_stream(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        step()
+        evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    launch_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    if dist is not None:
+        t = torch.tensor([elapsed, launch_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, launch_ms = float(t[0]), float(t[1])
+        tot = torch.tensor([ncells_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(tot)
+        ncells_total = int(tot[0])
+    else:
+        ncells_total = ncells_local
+
+    ms_per_step = elapsed / args.steps * 1e3
+    melem_s = ncells_total / (ms_per_step * 1e-3) / 1e6
+    achieved = B_E_P2_TET * ncells_local / (launch_ms * 1e-3) / 1e9  # per-GPU kernel GB/s (algorithmic)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        v, nc, t = cpu_baseline(args.cpu_sample_n, args.cpu_reps)
+        cpu = {"value": round(v, 4), "unit": "Melements/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/fa_oracle.c ora_assemble_elasticity (dolfinx assemble_cells + set_diagonal "
+                         f"restated), P2 tet, {args.cpu_sample_n}^3x6 = {nc} cells, zero+assemble+bc diag, "
+                         f"median of {args.cpu_reps} runs ({t:.2f} s each), 1 thread"}
+
+    if rank == 0:
+        out = {
+            "metric": "Melements/s assembled + achieved HBM GB/s, 3D P2 elasticity at 1/2/4/8 GPUs",
+            "value": round(melem_s, 3),
+            "unit": "Melements/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "hbm_GBps_algorithmic": round(achieved * world, 1),
+            "config": {"workload": f"config E mesh, linear elasticity J: unit cube {n}^3 x 6 Kuhn tets, P2 "
+                                   f"({ncells_total} cells, {(2 * n + 1) ** 3 * 3} dofs), E=E_range[cell%200], "
+                                   f"nu=0.3, x=0 clamped / x=1 prescribed, BSR(3) global matrix",
+                       "method": args.method, "quadrature_points": 4,
+                       "parallelism": f"z-slabs x{world}" if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel": "k_gather<3,10,4,4,2,0> (P2 tet row-gather)" if world == 1 else None,
+                         "bytes_per_cell": B_E_P2_TET, "launch_ms": round(launch_ms, 4)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

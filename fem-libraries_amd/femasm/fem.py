@@ -1,0 +1,508 @@
+"""dolfinx.fem-shaped host API over the femasm C ABI.
+
+Mirrors the calls the reference makes on its hot path (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:
+``create_functionspace`` :275-285, ``Function`` / ``Constant`` :253-262, :506-546,
+``locate_dofs_topological`` + ``DirichletBC`` :620-669, ``create_form`` :679-685,
+``petsc::create_matrix`` :688, ``assemble_matrix`` + ``set_diagonal`` :847-862), with the
+same argument meaning: bcs zero the rows/columns of constrained dofs and ``diagonal`` is
+inserted on them. Mesh, dofmaps, coefficients and the global BSR matrix are torch tensors
+on the GPU; every numeric step runs in hand-written HIP kernels (libfemasm.so). There is no
+CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from .la import MatrixCSR
+from .mesh import CellType, Mesh, NVERTS
+
+# basix reference sub-entities (edges as vertex pairs, hex faces as (v0, v1, v2))
+_EDGES = {
+    CellType.triangle: ((1, 2), (0, 2), (0, 1)),
+    CellType.tetrahedron: ((2, 3), (1, 3), (1, 2), (0, 3), (0, 2), (0, 1)),
+    CellType.quadrilateral: ((0, 1), (0, 2), (1, 3), (2, 3)),
+    CellType.hexahedron: ((0, 1), (0, 2), (0, 4), (1, 3), (1, 5), (2, 3), (2, 6), (3, 7), (4, 5), (4, 6), (5, 7), (6, 7)),
+}
+_HEX_FACES = ((0, 1, 2, 3), (0, 1, 4, 5), (0, 2, 4, 6), (1, 3, 5, 7), (2, 3, 6, 7), (4, 5, 6, 7))
+_HEX_FACE_SPAN = ((0, 1, 2), (0, 1, 4), (0, 2, 4), (1, 3, 5), (2, 3, 6), (4, 5, 6))
+_REF_VERTS = {
+    CellType.triangle: ((0, 0), (1, 0), (0, 1)),
+    CellType.tetrahedron: ((0, 0, 0), (1, 0, 0), (0, 1, 0), (0, 0, 1)),
+    CellType.quadrilateral: ((0, 0), (1, 0), (0, 1), (1, 1)),
+    CellType.hexahedron: tuple((b & 1, (b >> 1) & 1, (b >> 2) & 1) for b in range(8)),
+}
+
+
+def is_simplex(ct) -> bool:
+    return CellType(ct) in (CellType.triangle, CellType.tetrahedron)
+
+
+def num_nodes(ct, p: int) -> int:
+    ct = CellType(ct)
+    return {CellType.triangle: (p + 1) * (p + 2) // 2, CellType.tetrahedron: (p + 1) * (p + 2) * (p + 3) // 6,
+            CellType.quadrilateral: (p + 1) ** 2, CellType.hexahedron: (p + 1) ** 3}[ct]
+
+
+def line_points(p: int) -> np.ndarray:
+    """1-D node positions: equispaced (p <= 2) or GLL (p = 3; basix gll_warped)."""
+    if p == 3:
+        return np.array([0.0, 0.5 * (1 - 1 / np.sqrt(5)), 0.5 * (1 + 1 / np.sqrt(5)), 1.0])
+    return np.linspace(0.0, 1.0, p + 1)
+
+
+def node_lattice(ct, p: int) -> np.ndarray:
+    """basix local node -> integer lattice position (units of 1/p of the cell) [nn, tdim].
+    For tensor cells the entries are 1-D lattice indices (GLL positions at p = 3)."""
+    ct = CellType(ct)
+    V = np.array(_REF_VERTS[ct]) * p
+    out = [tuple(v) for v in V]
+    for a, b in _EDGES[ct]:
+        for s in range(1, p):
+            out.append(tuple(V[a] + s * (V[b] - V[a]) // p))
+    if ct == CellType.quadrilateral:
+        for i in range(1, p):
+            for j in range(1, p):
+                out.append((i, j))
+    if ct == CellType.hexahedron:
+        for f in _HEX_FACE_SPAN:
+            for s in range(1, p):
+                for t in range(1, p):
+                    out.append(tuple(V[f[0]] + s * (V[f[1]] - V[f[0]]) // p + t * (V[f[2]] - V[f[0]]) // p))
+        for i in range(1, p):
+            for j in range(1, p):
+                for k in range(1, p):
+                    out.append((i, j, k))
+    if is_simplex(ct) and p > 2:
+        raise NotImplementedError("simplex degree > 2")
+    return np.array(out, dtype=np.int64)
+
+
+def reference_nodes(ct, p: int) -> np.ndarray:
+    L = node_lattice(ct, p)
+    if is_simplex(ct):
+        return L.astype(np.float64) / p
+    return line_points(p)[L]
+
+
+def _geometry_basis(ct, X: np.ndarray) -> np.ndarray:
+    """P1 / Q1 geometry basis values at reference points X [n, tdim] -> [n, nverts]."""
+    ct = CellType(ct)
+    if is_simplex(ct):
+        return np.concatenate([1.0 - X.sum(1, keepdims=True), X], axis=1)
+    cols = []
+    for v in _REF_VERTS[ct]:
+        f = np.ones(X.shape[0])
+        for d, bit in enumerate(v):
+            f = f * (X[:, d] if bit else 1.0 - X[:, d])
+        cols.append(f)
+    return np.stack(cols, 1)
+
+
+class FunctionSpace:
+    """Vector (bs = gdim) or scalar Lagrange space, or DG0 (per-cell) space."""
+
+    def __init__(self, mesh: Mesh, family: str, degree: int, shape: tuple | None):
+        self.mesh = mesh
+        self.family = family
+        self.degree = int(degree)
+        self.bs = int(np.prod(shape)) if shape else 1
+        self._adjacency = None
+        self._pattern = None
+        if family in ("DG", "Discontinuous Lagrange"):
+            if degree != 0:
+                raise NotImplementedError("only DG0 coefficient spaces")
+            self.dofmap = torch.arange(mesh.num_cells, dtype=torch.int32, device=mesh.device).reshape(-1, 1)
+            self.num_nodes = mesh.num_cells
+            self.nn = 1
+            return
+        if family not in ("Lagrange", "P", "Q", "CG"):
+            raise ValueError(f"unsupported family {family}")
+        self.nn = num_nodes(mesh.cell_type, self.degree)
+        if self.degree == 1:
+            self.dofmap = mesh.cells
+            self.num_nodes = mesh.num_vertices
+        elif mesh.structured is not None:
+            self.dofmap, self.num_nodes = _structured_dofmap(mesh, self.degree)
+        else:
+            self.dofmap, self.num_nodes = _generic_dofmap(mesh, self.degree)
+        self._x = None
+
+    @property
+    def num_dofs(self) -> int:
+        return self.num_nodes * self.bs
+
+    def tabulate_dof_coordinates(self) -> torch.Tensor:
+        """Node coordinates [num_nodes, gdim] (the geometry map applied to the reference nodes)."""
+        if self._x is None and self.mesh.structured is not None and self.degree > 1:
+            self._x = _structured_node_coordinates(self.mesh, self.degree)
+        if self._x is None:
+            m = self.mesh
+            X = reference_nodes(m.cell_type, self.degree)
+            Psi = torch.tensor(_geometry_basis(m.cell_type, X), dtype=torch.float64, device=m.device)  # [nn, nv]
+            xv = m.x[m.cells.to(torch.int64)]  # [nc, nv, gdim]
+            xn = torch.einsum("kv,cvd->ckd", Psi, xv)
+            out = torch.zeros((self.num_nodes, m.gdim), dtype=torch.float64, device=m.device)
+            out[self.dofmap.to(torch.int64).reshape(-1)] = xn.reshape(-1, m.gdim)
+            self._x = out
+        return self._x
+
+    # native objects -------------------------------------------------------------------
+    def _fa_mesh(self) -> _lib.fa_mesh:
+        m = self.mesh
+        s = _lib.fa_mesh()
+        s.cell_type = int(m.cell_type)
+        s.degree = self.degree
+        s.gdim = m.gdim
+        s.nn = self.nn
+        s.ncells = m.num_cells
+        s.nnodes = self.num_nodes
+        s.cells = self.dofmap.data_ptr()
+        s.nv = NVERTS[m.cell_type]
+        s.geom = m.cells.data_ptr()
+        s.x = m.x.data_ptr()
+        return s
+
+    def adjacency(self):
+        """Node -> cell adjacency (built once on the GPU: fa_build_adjacency)."""
+        if self._adjacency is None:
+            L = _lib.load()
+            dev = self.mesh.device
+            ptr = torch.empty(self.num_nodes + 1, dtype=torch.int64, device=dev)
+            idx = torch.empty(self.mesh.num_cells * self.nn, dtype=torch.int32, device=dev)
+            fm = self._fa_mesh()
+            _lib.check(L.fa_build_adjacency(ctypes.byref(fm), ptr.data_ptr(), idx.data_ptr(), _lib.stream_handle(dev)),
+                       "fa_build_adjacency")
+            self._adjacency = (ptr, idx)
+        return self._adjacency
+
+    def _fa_adjacency(self) -> _lib.fa_adjacency:
+        ptr, idx = self.adjacency()
+        a = _lib.fa_adjacency()
+        a.ptr = ptr.data_ptr()
+        a.idx = idx.data_ptr()
+        return a
+
+
+def _structured_dofmap(mesh: Mesh, p: int, chunk: int = 1 << 22):
+    """Lattice numbering of a structured mesh's degree-p nodes: node index of lattice point
+    (I, J[, K]) is I + (p nx + 1)(J + (p ny + 1) K) — neighbours stay close in memory.
+    Processed in cell chunks to bound temporaries (config E has 50 M cells)."""
+    st = mesh.structured
+    n = st["n"]
+    tdim = len(n)
+    dims = [p * k + 1 for k in n]
+    vdims = [k + 1 for k in n]
+    dev = mesh.device
+    L = torch.tensor(node_lattice(mesh.cell_type, p), dtype=torch.int64, device=dev)  # [nn, tdim]
+    out = torch.empty((mesh.num_cells, L.shape[0]), dtype=torch.int32, device=dev)
+    simplex = is_simplex(mesh.cell_type)
+    for c0 in range(0, mesh.num_cells, chunk):
+        v = mesh.cells[c0:c0 + chunk].to(torch.int64)
+        vlat = []
+        for d in range(tdim):
+            stride = int(np.prod(vdims[:d]))
+            vlat.append((v // stride) % vdims[d])
+        vlat = torch.stack(vlat, -1)  # [nc, nv, tdim]
+        v0 = vlat[:, 0, :]
+        nl = p * v0[:, None, :]
+        if simplex:
+            # node lattice = p v0 + sum_k L[node, k] (v_k - v0)   (L in units of 1/p)
+            for k in range(tdim):
+                nl = nl + L[None, :, k, None] * (vlat[:, k + 1, :] - v0)[:, None, :]
+        else:
+            nl = nl + L[None, :, :]
+        idx = torch.zeros(nl.shape[:2], dtype=torch.int64, device=dev)
+        for d in range(tdim - 1, -1, -1):
+            idx = idx * dims[d] + nl[:, :, d]
+        out[c0:c0 + chunk] = idx.to(torch.int32)
+    return out.contiguous(), int(np.prod(dims))
+
+
+def _structured_node_coordinates(mesh: Mesh, p: int) -> torch.Tensor:
+    """Node coordinates of the lattice numbering (uniform box, GLL-graded inside cells at p = 3)."""
+    st = mesh.structured
+    n, lengths = st["n"], st["lengths"]
+    r = torch.tensor(line_points(p), dtype=torch.float64, device=mesh.device)
+    axes = []
+    for k, Lk in zip(n, lengths):
+        i = torch.arange(p * k + 1, device=mesh.device)
+        cell, loc = torch.div(i, p, rounding_mode="floor"), i % p
+        cell = torch.where(i == p * k, torch.full_like(cell, k - 1), cell)
+        loc = torch.where(i == p * k, torch.full_like(loc, p), loc)
+        axes.append((cell.to(torch.float64) + r[loc]) * (Lk / k))
+    grids = torch.meshgrid(*reversed(axes), indexing="ij")
+    return torch.stack([g.reshape(-1) for g in reversed(grids)], 1).contiguous()
+
+
+def _generic_dofmap(mesh: Mesh, p: int):
+    """Degree-2 numbering of an unstructured mesh: vertices, then one node per edge (and per
+    hex face and quad/hex cell), edges identified by their sorted vertex pair."""
+    if p != 2:
+        raise NotImplementedError("unstructured meshes: degree <= 2 (Q3 needs a structured mesh)")
+    ct = mesh.cell_type
+    c = mesh.cells.to(torch.int64)
+    nv = mesh.num_vertices
+    parts = [c]
+    E = torch.tensor(_EDGES[ct], dtype=torch.int64, device=c.device)
+    ev = c[:, E]  # [nc, ne, 2]
+    lo, hi = ev.min(-1).values, ev.max(-1).values
+    key = lo * nv + hi
+    uniq, inv = torch.unique(key.reshape(-1), return_inverse=True)
+    parts.append(nv + inv.reshape(key.shape))
+    nxt = nv + uniq.numel()
+    if ct == CellType.hexahedron:
+        F = torch.tensor(_HEX_FACES, dtype=torch.int64, device=c.device)
+        fv = torch.sort(c[:, F], dim=-1).values  # [nc, 6, 4]
+        fu, finv = torch.unique(fv.reshape(-1, 4), dim=0, return_inverse=True)
+        parts.append(nxt + finv.reshape(fv.shape[:2]))
+        nxt += fu.shape[0]
+    if ct in (CellType.quadrilateral, CellType.hexahedron):
+        parts.append(nxt + torch.arange(mesh.num_cells, device=c.device).reshape(-1, 1))
+        nxt += mesh.num_cells
+    return torch.cat(parts, 1).to(torch.int32).contiguous(), int(nxt)
+
+
+def functionspace(mesh: Mesh, element) -> FunctionSpace:
+    """dolfinx.fem.functionspace(mesh, ("Lagrange", p, (gdim,))) / ("DG", 0)."""
+    family, degree = element[0], element[1]
+    shape = element[2] if len(element) > 2 else None
+    return FunctionSpace(mesh, family, degree, shape)
+
+
+class Function:
+    def __init__(self, V: FunctionSpace, name: str = "f", x: torch.Tensor | None = None):
+        self.function_space = V
+        self.name = name
+        n = V.num_nodes * V.bs
+        self.x = x if x is not None else torch.zeros(n, dtype=torch.float64, device=V.mesh.device)
+
+    @property
+    def array(self) -> torch.Tensor:
+        return self.x
+
+    def interpolate(self, fn):
+        """Nodal interpolation: fn(x[gdim, n]) -> values [bs, n] (dolfinx convention)."""
+        V = self.function_space
+        xn = V.tabulate_dof_coordinates()
+        vals = fn(xn.T)
+        vals = torch.as_tensor(vals, dtype=torch.float64, device=xn.device).reshape(V.bs, -1)
+        self.x = vals.T.contiguous().reshape(-1)
+
+
+class Constant:
+    def __init__(self, mesh_or_value, value=None):
+        self.value = float(mesh_or_value if value is None else value)
+
+    def __float__(self):
+        return self.value
+
+
+@dataclass
+class DirichletBC:
+    """Constrained dofs of V with their prescribed values (blocked dof = node*bs + comp)."""
+    V: FunctionSpace
+    dofs: torch.Tensor  # int64 dof indices
+    g: torch.Tensor  # float64 [num_dofs] prescribed values (0 elsewhere)
+
+    def marker(self) -> torch.Tensor:
+        m = torch.zeros(self.V.num_dofs, dtype=torch.int8, device=self.dofs.device)
+        m[self.dofs] = 1
+        return m
+
+
+def locate_dofs_geometrical(V: FunctionSpace, marker) -> torch.Tensor:
+    """Nodes whose coordinates satisfy marker(x[gdim, n]); returns node indices (int64)."""
+    xn = V.tabulate_dof_coordinates()
+    return torch.nonzero(marker(xn.T), as_tuple=False).reshape(-1)
+
+
+def dirichletbc(value, nodes: torch.Tensor, V: FunctionSpace, components=None) -> DirichletBC:
+    """Constrain all (or the given) components of `nodes` to `value` (a scalar or a bs-vector)."""
+    bs = V.bs
+    comps = list(range(bs)) if components is None else list(components)
+    val = torch.as_tensor(value, dtype=torch.float64, device=nodes.device).reshape(-1)
+    if val.numel() == 1:
+        val = val.expand(bs)
+    nodes = nodes.to(torch.int64)
+    dofs = torch.cat([nodes * bs + c for c in comps]) if nodes.numel() else nodes
+    g = torch.zeros(V.num_dofs, dtype=torch.float64, device=nodes.device)
+    for c in comps:
+        g[nodes * bs + c] = val[c]
+    return DirichletBC(V, dofs, g)
+
+
+def _combine_bcs(V: FunctionSpace, bcs):
+    if not bcs:
+        return None, None
+    marker = torch.zeros(V.num_dofs, dtype=torch.int8, device=V.mesh.device)
+    g = torch.zeros(V.num_dofs, dtype=torch.float64, device=V.mesh.device)
+    for bc in bcs:
+        marker[bc.dofs] = 1
+        g[bc.dofs] = bc.g[bc.dofs]
+    return marker, g
+
+
+# ---------------------------------------------------------------------------------- forms
+class LinearElasticity:
+    """J of the reference form with damage d = 0:
+    inner(sigma(du), eps(v)) dx, sigma = lmbda tr(eps) I + 2 mu eps, mu = E/(2(1+nu)),
+    lmbda = E nu/((1+nu)(1-2nu))  (FEniCSx/mechanic2d/asym_ufl.py:22-34, :78-83).
+    E: DG0 Function / per-cell tensor / float; nu: Constant / float. Alternatively lam & mu per cell."""
+    kind = _lib.FA_LINEAR_ELASTICITY
+
+    def __init__(self, V: FunctionSpace, E=None, nu=0.3, lam=None, mu=None, quadrature_degree: int | None = None):
+        self.V = V
+        nc = V.mesh.num_cells
+        dev = V.mesh.device
+        self.nu = float(nu)
+        self.E = self.lam = self.mu = None
+        if E is not None:
+            self.E = _cellwise(E, nc, dev)
+        else:
+            self.lam, self.mu = _cellwise(lam, nc, dev), _cellwise(mu, nc, dev)
+        self.qdeg = -1 if quadrature_degree is None else int(quadrature_degree)
+        self.u = self.d = self.f = None
+
+
+class AsymDamage(LinearElasticity):
+    """The reference mechanic2d J: derivative of inner(sigma(u), eps(v)) dxx with the
+    asymmetric tension/compression damage law, P1 triangles, one quadrature point
+    (FEniCSx/mechanic2d/asym_ufl.py:36-81; MFEM/mechanic2d/asym_elasto_damage_model.cc:639-916).
+    u: displacement Function, d: damage (P1 scalar Function or per-node tensor)."""
+    kind = _lib.FA_ASYM_DAMAGE
+
+    def __init__(self, V: FunctionSpace, E=None, nu=0.3, u=None, d=None, lam=None, mu=None):
+        super().__init__(V, E=E, nu=nu, lam=lam, mu=mu, quadrature_degree=1)
+        self.u = None if u is None else (u.x if isinstance(u, Function) else u)
+        self.d = None if d is None else (d.x if isinstance(d, Function) else d)
+
+
+def _cellwise(v, nc, dev):
+    if isinstance(v, Function):
+        v = v.x
+    t = torch.as_tensor(v, dtype=torch.float64, device=dev)
+    if t.numel() == 1:
+        t = t.reshape(1).expand(nc)
+    return t.contiguous()
+
+
+def form(a):
+    """dolfinx.fem.form analogue: forms are ready-made descriptors here (no code generation);
+    returns the argument after validating it."""
+    if not isinstance(a, LinearElasticity):
+        raise TypeError("expected a femasm form descriptor (LinearElasticity, AsymDamage, ...)")
+    return a
+
+
+def _fa_form(a) -> _lib.fa_form:
+    f = _lib.fa_form()
+    f.kind = a.kind
+    f.qdeg = a.qdeg
+    f.E = _lib.ptr(a.E)
+    f.nu = a.nu
+    f.lam = _lib.ptr(a.lam)
+    f.mu = _lib.ptr(a.mu)
+    f.u = _lib.ptr(a.u)
+    f.d = _lib.ptr(a.d)
+    f.f = _lib.ptr(a.f)
+    return f
+
+
+def create_matrix(a) -> MatrixCSR:
+    """Sparsity pattern of the bilinear form (all node pairs of every cell), built on the GPU
+    (dolfinx.fem.petsc.create_matrix, FEniCSx/mechanic2d/asym_elasto_damage_model.cc:688)."""
+    V = a.V
+    if V._pattern is None:
+        L = _lib.load()
+        dev = V.mesh.device
+        fm = V._fa_mesh()
+        adj = V._fa_adjacency()
+        indptr = torch.empty(V.num_nodes + 1, dtype=torch.int64, device=dev)
+        nb = ctypes.c_int64(0)
+        sh = _lib.stream_handle(dev)
+        _lib.check(L.fa_sparsity_count(ctypes.byref(fm), ctypes.byref(adj), indptr.data_ptr(), ctypes.byref(nb), sh),
+                   "fa_sparsity_count")
+        indices = torch.empty(nb.value, dtype=torch.int32, device=dev)
+        _lib.check(L.fa_sparsity_fill(ctypes.byref(fm), ctypes.byref(adj), indptr.data_ptr(), indices.data_ptr(), sh),
+                   "fa_sparsity_fill")
+        V._pattern = (indptr, indices)
+    indptr, indices = V._pattern
+    return MatrixCSR(indptr, indices, V.bs)
+
+
+def _fa_bsr(A: MatrixCSR) -> _lib.fa_bsr:
+    b = _lib.fa_bsr()
+    b.nrows = A.num_block_rows
+    b.bs = A.bs
+    b.nblocks = A.num_blocks
+    b.indptr = A.indptr.data_ptr()
+    b.indices = A.indices.data_ptr()
+    b.data = A.data.data_ptr()
+    return b
+
+
+def gather_plan(V: FunctionSpace, A: MatrixCSR):
+    """Row-chunk plan of the gather kernel for A's pattern (cached on the matrix)."""
+    plan = V.__dict__.get("_plan")
+    if plan is None or plan[2] is not A.indptr:
+        L = _lib.load()
+        fm = V._fa_mesh()
+        adj = V._fa_adjacency()
+        fb = _fa_bsr(A)
+        rs = torch.empty(V.num_nodes + 1, dtype=torch.int64, device=V.mesh.device)
+        plan = _lib.fa_plan()
+        _lib.check(L.fa_plan_gather(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), rs.data_ptr(),
+                                    ctypes.byref(plan), _lib.stream_handle(V.mesh.device)), "fa_plan_gather")
+        V._plan = (plan, rs, A.indptr)
+        plan = V._plan
+    return plan[0]
+
+
+def assemble_matrix(a, bcs=None, diagonal: float = 1.0, A: MatrixCSR | None = None, method: str = "gather") -> MatrixCSR:
+    """Assemble the bilinear form into a BSR matrix (dolfinx.fem.assemble_matrix + set_diagonal).
+
+    bcs: list of DirichletBC — their rows and columns receive no cell contribution and their
+    diagonal entries are set to `diagonal`. method: "gather" (row-gather, default) or
+    "scatter" (element scatter with FP64 atomics; zeroes A first like MatZeroEntries).
+    """
+    V = a.V
+    if A is None:
+        A = create_matrix(a)
+    L = _lib.load()
+    marker, _ = _combine_bcs(V, bcs)
+    fm = V._fa_mesh()
+    ff = _fa_form(a)
+    fb = _fa_bsr(A)
+    sh = _lib.stream_handle(V.mesh.device)
+    if method == "gather":
+        adj = V._fa_adjacency()
+        plan = gather_plan(V, A)
+        rc = L.fa_assemble_matrix(ctypes.byref(fm), ctypes.byref(ff), ctypes.byref(adj), ctypes.byref(plan),
+                                  _lib.ptr(marker), float(diagonal), ctypes.byref(fb), _lib.FA_GATHER, sh)
+    elif method == "scatter":
+        rc = L.fa_assemble_matrix(ctypes.byref(fm), ctypes.byref(ff), None, None, _lib.ptr(marker), float(diagonal),
+                                  ctypes.byref(fb), _lib.FA_SCATTER | _lib.FA_ZERO_FIRST, sh)
+    else:
+        raise ValueError(f"unknown method {method}")
+    _lib.check(rc, "fa_assemble_matrix")
+    A._keepalive = (marker, a)
+    return A
+
+
+def tabulate_cells(a, c0: int = 0, ncells: int | None = None) -> torch.Tensor:
+    """Element matrices [nc, nn*bs, nn*bs] (batched ffcx tabulate_tensor / AssembleElementGrad)."""
+    V = a.V
+    nc = V.mesh.num_cells - c0 if ncells is None else ncells
+    nd = V.nn * V.bs
+    Ae = torch.empty((nc, nd, nd), dtype=torch.float64, device=V.mesh.device)
+    L = _lib.load()
+    fm = V._fa_mesh()
+    ff = _fa_form(a)
+    _lib.check(L.fa_tabulate_cells(ctypes.byref(fm), ctypes.byref(ff), c0, nc, Ae.data_ptr(),
+                                   _lib.stream_handle(V.mesh.device)), "fa_tabulate_cells")
+    return Ae

@@ -1,0 +1,162 @@
+/*
+ * femasm — MI355X (gfx950) element-stiffness assembly, C ABI.
+ *
+ * The drop-in boundary for the reference's hot path (SalzmanA/fem-libraries, mechanic2d):
+ * the per-cell B^T.D.B quadrature contraction and its scatter into a global sparse matrix.
+ * All pointers are DEVICE pointers (hipMalloc / torch.cuda tensors) unless stated; every
+ * call is asynchronous on `stream` (a hipStream_t; NULL = the default stream) unless it
+ * returns a size the host needs, which is stated per function.  Buffers are owned by the
+ * caller; the library allocates only stream-ordered scratch that it frees before returning.
+ * Errors: every function returns FA_OK (0) or a negative FA_E_* code and sets a
+ * thread-local message readable with fa_last_error().  Calls are re-entrant across streams.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo):
+ *   fa_tabulate_cells    ufcx `tabulate_tensor_float64` of the ffcx-compiled J form
+ *                        (form built at FEniCSx/mechanic2d/asym_elasto_damage_model.cc:684-685
+ *                        from FEniCSx/mechanic2d/asym_ufl.py:83) and MFEM
+ *                        damIntegrator::AssembleElementGrad
+ *                        (MFEM/mechanic2d/asym_elasto_damage_model.cc:639-916), batched over cells.
+ *   fa_assemble_matrix   dolfinx::fem::assemble_matrix(set_block_fn(A, ADD_VALUES), J_form, {bcl,bcr})
+ *                        + fem::set_diagonal(..., 1.0) as called from the setJ callback
+ *                        (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:847-862); MFEM
+ *                        NonlinearForm::GetGradient driven from :1546.
+ *   fa_build_adjacency,  dolfinx::fem::petsc::create_matrix(J_form) — the sparsity pattern of
+ *   fa_sparsity_count,   (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:688).
+ *   fa_sparsity_fill
+ *   fa_assemble_vector   dolfinx::fem::assemble_vector(b, F_form)
+ *                        (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:825) and MFEM
+ *                        damIntegrator::AssembleElementVector (:559-637).
+ *   fa_apply_lifting,    dolfinx::fem::apply_lifting / set_bc as called from setF
+ *   fa_set_bc            (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:827, :836).
+ */
+#ifndef FEMASM_H
+#define FEMASM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FA_OK 0
+#define FA_E_ARG (-1)       /* invalid argument (null pointer, bad size) */
+#define FA_E_UNSUPPORTED (-2) /* element / form / quadrature combination not implemented */
+#define FA_E_HIP (-3)       /* HIP runtime error (launch, allocation) */
+#define FA_E_PATTERN (-4)   /* sparsity pattern missing an entry the mesh needs */
+#define FA_E_CAPACITY (-5)  /* a row exceeds a kernel capacity (reported with sizes) */
+
+/* dolfinx::mesh::CellType values */
+#define FA_TRIANGLE 3
+#define FA_QUADRILATERAL 4
+#define FA_TETRAHEDRON (-4)
+#define FA_HEXAHEDRON 8
+
+/* Form kinds */
+#define FA_LINEAR_ELASTICITY 0 /* sigma = lambda tr(eps) I + 2 mu eps  (reference J with d = 0) */
+#define FA_ASYM_DAMAGE 1       /* reference mechanic2d damage law, P1 triangles (2-D plane strain) */
+#define FA_NEO_HOOKEAN 2       /* compressible neo-Hookean, AD tangent */
+
+/* fa_assemble_matrix flags */
+#define FA_GATHER 0x0        /* row-gather: each BSR row computed once, plain coalesced stores */
+#define FA_SCATTER 0x1       /* element-scatter with FP64 atomics (dolfinx/PETSc ADD_VALUES shape) */
+#define FA_ZERO_FIRST 0x2    /* FA_SCATTER only: zero A->data first (MatZeroEntries) */
+
+typedef struct {
+  int32_t cell_type;     /* FA_TRIANGLE ... */
+  int32_t degree;        /* Lagrange degree of the vector space (1, 2, 3) */
+  int32_t gdim;          /* geometric dim = topological dim = block size bs (2 or 3) */
+  int32_t nn;            /* nodes per cell of the space: dofmap width */
+  int64_t ncells;
+  int64_t nnodes;        /* number of space nodes (BSR block rows) */
+  const int32_t* cells;  /* [ncells][nn] node dofmap, basix local ordering */
+  int32_t nv;            /* geometry nodes per cell (P1 / Q1 vertices) */
+  int32_t _pad;
+  const int32_t* geom;   /* [ncells][nv] geometry dofmap */
+  const double* x;       /* [nverts][gdim] vertex coordinates */
+} fa_mesh;
+
+typedef struct {
+  int32_t kind;          /* FA_LINEAR_ELASTICITY ... */
+  int32_t qdeg;          /* quadrature degree; < 0 = the degree UFL estimates for the form */
+  const double* E;       /* [ncells] Young's modulus (DG0), or NULL to use lam/mu */
+  double nu;             /* Poisson ratio (Constant) when E != NULL */
+  const double* lam;     /* [ncells] Lame lambda when E == NULL */
+  const double* mu;      /* [ncells] Lame mu when E == NULL */
+  const double* u;       /* [nnodes*bs] state (damage, neo-Hookean, residual); may be NULL */
+  const double* d;       /* [nnodes] damage (P1) for FA_ASYM_DAMAGE; may be NULL (= 0) */
+  const double* f;       /* [nnodes*bs] body force (residual); may be NULL */
+} fa_form;
+
+typedef struct {
+  int64_t nrows;         /* block rows = mesh nnodes */
+  int32_t bs;            /* block size = gdim */
+  int32_t _pad;
+  int64_t nblocks;       /* indices length */
+  const int64_t* indptr; /* [nrows+1] */
+  const int32_t* indices;/* [nblocks], sorted per row */
+  double* data;          /* [nblocks][bs][bs] row-major blocks */
+} fa_bsr;
+
+typedef struct {
+  const int64_t* ptr;    /* [nnodes+1] */
+  const int32_t* idx;    /* [ncells*nn] flat dofmap positions p = cell*nn + local, sorted per node */
+} fa_adjacency;
+
+/* Row-chunk plan for the gather kernel (host-computed once per pattern). */
+typedef struct {
+  int64_t nchunks;
+  const int64_t* row_start;  /* device [nchunks+1] */
+  int32_t max_blocks;        /* largest block count of a chunk */
+  int32_t max_adj;           /* largest adjacency count of a chunk */
+} fa_plan;
+
+const char* fa_last_error(void);
+int fa_version(void);
+
+/* Element metadata: nodes per cell and quadrature points for (cell_type, degree, qdeg). */
+int fa_element_info(int32_t cell_type, int32_t degree, int32_t qdeg, int32_t* nn, int32_t* nq);
+
+/* Node -> cell adjacency (transpose of the dofmap): ptr [nnodes+1], idx [ncells*nn]. */
+int fa_build_adjacency(const fa_mesh* mesh, int64_t* ptr, int32_t* idx, void* stream);
+
+/* BSR sparsity: pass 1 writes indptr [nnodes+1] and returns the block count in *nblocks
+ * (synchronises `stream` to read it); pass 2 fills indices [nblocks] sorted per row. */
+int fa_sparsity_count(const fa_mesh* mesh, const fa_adjacency* adj, int64_t* indptr, int64_t* nblocks, void* stream);
+int fa_sparsity_fill(const fa_mesh* mesh, const fa_adjacency* adj, const int64_t* indptr, int32_t* indices, void* stream);
+
+/* Gather plan: row chunks whose blocks and adjacency fit the kernel's LDS budget.
+ * row_start is a caller-owned device buffer of capacity nnodes+1; nchunks etc. returned
+ * in *plan (synchronises `stream`). */
+int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int64_t* row_start, fa_plan* plan,
+                   void* stream);
+
+/* Per-cell element matrices Ae [ncells_out][nn*bs][nn*bs] (dof = node*bs + comp) for cells
+ * [c0, c0+ncells_out) — the batched ufcx tabulate_tensor / AssembleElementGrad. */
+int fa_tabulate_cells(const fa_mesh* mesh, const fa_form* form, int64_t c0, int64_t ncells_out, double* Ae,
+                      void* stream);
+
+/* Global matrix assembly into A (BSR, pattern from fa_sparsity_*). bc: int8 per dof
+ * (node*bs+comp) or NULL. Entries in bc rows/columns get no cell contribution and bc
+ * diagonal entries are set to `diag` (dolfinx assemble_matrix + set_diagonal).
+ * FA_GATHER needs adj and plan; FA_SCATTER needs neither (plan may be NULL). */
+int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, const fa_adjacency* adj, const fa_plan* plan,
+                       const int8_t* bc, double diag, fa_bsr* A, int32_t flags, void* stream);
+
+/* Residual b += int sigma(u):eps(v) - f.v over all cells (b is ADDED into; zero it first). */
+int fa_assemble_vector(const fa_mesh* mesh, const fa_form* form, double* b, void* stream);
+
+/* dolfinx apply_lifting with one form: b[i] -= alpha * sum_j A_ij (g_j - x0_j) over bc
+ * columns j, computed cell by cell with the cell matrices (bc rows i get no contribution;
+ * set_bc overwrites them). The reference calls it with alpha = -1
+ * (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:827). g, x0 per dof (x0 may be NULL = 0). */
+int fa_apply_lifting(const fa_mesh* mesh, const fa_form* form, double* b, const int8_t* bc, const double* g,
+                     const double* x0, double alpha, void* stream);
+
+/* b[i] = alpha * (g[i] - x0[i]) on bc dofs (x0 may be NULL). ndofs = nnodes*bs. */
+int fa_set_bc(double* b, int64_t ndofs, const int8_t* bc, const double* g, const double* x0, double alpha,
+              void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FEMASM_H */

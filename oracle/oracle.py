@@ -1,0 +1,219 @@
+"""ORACLE — test infrastructure only.
+
+numpy/ctypes front end of ``oracle/fa_oracle.c``, the CPU restatement of the reference's
+assembly path (see that file's header for the reference anchors and the pinning status).
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg import
+this module; the product package ``fem-libraries_amd/femasm`` never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libfa_oracle.so")
+
+TRI, QUAD, TET, HEX = 3, 4, -4, 8
+_GDIM = {TRI: 2, QUAD: 2, TET: 3, HEX: 3}
+_NVERT = {TRI: 3, QUAD: 4, TET: 4, HEX: 8}
+
+
+def build() -> str:
+    """Compile the oracle with its Makefile (gcc); returns the .so path."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+class _Mesh(ctypes.Structure):
+    _fields_ = [
+        ("cell_type", ctypes.c_int),
+        ("degree", ctypes.c_int),
+        ("gdim", ctypes.c_int),
+        ("ncells", ctypes.c_int64),
+        ("nn", ctypes.c_int),
+        ("cells", ctypes.c_void_p),
+        ("nv", ctypes.c_int),
+        ("geom", ctypes.c_void_p),
+        ("x", ctypes.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.c_void_p
+        L.ora_num_nodes.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.ora_nodes.argtypes = [ctypes.c_int, ctypes.c_int, P]
+        L.ora_tabulate.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P]
+        L.ora_quadrature.argtypes = [ctypes.c_int, ctypes.c_int, P, P]
+        L.ora_damage_hook.argtypes = [P, ctypes.c_double, ctypes.c_double, ctypes.c_double, P]
+        L.ora_damage_stress.argtypes = [P, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, P]
+        L.ora_sparsity.argtypes = [ctypes.c_int64, ctypes.c_int, P, ctypes.c_int64, P, P]
+        L.ora_sparsity.restype = ctypes.c_int64
+        L.ora_assemble_elasticity.argtypes = [ctypes.POINTER(_Mesh), P, P, ctypes.c_int, P, ctypes.c_double, P, P, P]
+        L.ora_assemble_damage.argtypes = [ctypes.POINTER(_Mesh), P, P, P, P, P, ctypes.c_double, P, P, P]
+        L.ora_cell_matrices_elasticity.argtypes = [ctypes.POINTER(_Mesh), P, P, ctypes.c_int, P]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def nodes(cell_type: int, degree: int) -> np.ndarray:
+    X = np.zeros((64, 3))
+    n = lib().ora_nodes(cell_type, degree, _p(X))
+    assert n > 0
+    return X[:n, : _GDIM[cell_type]].copy()
+
+
+def quadrature(cell_type: int, degree: int):
+    pts = np.zeros((512, 3))
+    w = np.zeros(512)
+    nq = lib().ora_quadrature(cell_type, degree, _p(pts), _p(w))
+    td = _GDIM[cell_type]
+    return np.ascontiguousarray(pts.reshape(-1)[: nq * td].reshape(nq, td)), w[:nq].copy()
+
+
+def tabulate(cell_type: int, degree: int, pts: np.ndarray):
+    pts = np.ascontiguousarray(pts, dtype=np.float64)
+    npts, td = pts.shape
+    nn = lib().ora_num_nodes(cell_type, degree)
+    vals = np.zeros((npts, nn))
+    grads = np.zeros((npts, nn, td))
+    r = lib().ora_tabulate(cell_type, degree, npts, _p(pts), _p(vals), _p(grads))
+    assert r == nn
+    return vals, grads
+
+
+def damage_hook(strain, lam, mu, d):
+    s = np.ascontiguousarray(strain, dtype=np.float64)
+    h = np.zeros(9)
+    lib().ora_damage_hook(_p(s), lam, mu, d, _p(h))
+    return h.reshape(3, 3)
+
+
+def damage_stress(strain, lam, mu, d, w=1.0):
+    s = np.ascontiguousarray(strain, dtype=np.float64)
+    out = np.zeros(3)
+    lib().ora_damage_stress(_p(s), lam, mu, d, w, _p(out))
+    return out
+
+
+def sparsity(cells: np.ndarray, nnodes: int):
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    nc, nn = cells.shape
+    indptr = np.zeros(nnodes + 1, dtype=np.int64)
+    nb = lib().ora_sparsity(nc, nn, _p(cells), nnodes, _p(indptr), None)
+    assert nb >= 0
+    indices = np.zeros(nb, dtype=np.int32)
+    lib().ora_sparsity(nc, nn, _p(cells), nnodes, _p(indptr), _p(indices))
+    return indptr, indices
+
+
+def _mesh_struct(cell_type, degree, cells, geom, x):
+    m = _Mesh()
+    m.cell_type = cell_type
+    m.degree = degree
+    m.gdim = _GDIM[cell_type]
+    m.ncells = cells.shape[0]
+    m.nn = cells.shape[1]
+    m.cells = cells.ctypes.data
+    m.nv = geom.shape[1]
+    m.geom = geom.ctypes.data
+    m.x = x.ctypes.data
+    return m
+
+
+def lame(E, nu):
+    """Lamé parameters from Young's modulus and Poisson ratio
+    (FEniCSx/mechanic2d/asym_ufl.py:26-27)."""
+    E = np.asarray(E, dtype=np.float64)
+    mu = E / (2.0 * (1.0 + nu))
+    lmbda = E * nu / ((1.0 + nu) * (1.0 - 2.0 * nu))
+    return lmbda, mu
+
+
+def assemble_elasticity(cell_type, degree, cells, geom, x, lam, mu, indptr, indices, bc=None, diag=1.0, qdeg=-1):
+    """dolfinx-semantics matrix assembly into BSR (blocks gdim x gdim). Returns values [nb, bs, bs]."""
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    geom = np.ascontiguousarray(geom, dtype=np.int32)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    lam = np.ascontiguousarray(np.broadcast_to(lam, (cells.shape[0],)), dtype=np.float64)
+    mu = np.ascontiguousarray(np.broadcast_to(mu, (cells.shape[0],)), dtype=np.float64)
+    bs = _GDIM[cell_type]
+    vals = np.zeros((indices.shape[0], bs, bs))
+    m = _mesh_struct(cell_type, degree, cells, geom, x)
+    bcp = None
+    if bc is not None:
+        bc = np.ascontiguousarray(bc, dtype=np.int8)
+        bcp = _p(bc)
+    r = lib().ora_assemble_elasticity(ctypes.byref(m), _p(lam), _p(mu), qdeg, bcp, diag, _p(indptr), _p(indices), _p(vals))
+    assert r == 0, r
+    return vals
+
+
+def assemble_damage(cells, geom, x, lam, mu, u, dnode, indptr, indices, bc=None, diag=1.0):
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    geom = np.ascontiguousarray(geom, dtype=np.int32)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    lam = np.ascontiguousarray(np.broadcast_to(lam, (cells.shape[0],)), dtype=np.float64)
+    mu = np.ascontiguousarray(np.broadcast_to(mu, (cells.shape[0],)), dtype=np.float64)
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    dnode = np.ascontiguousarray(dnode, dtype=np.float64)
+    vals = np.zeros((indices.shape[0], 2, 2))
+    m = _mesh_struct(TRI, 1, cells, geom, x)
+    bcp = None
+    if bc is not None:
+        bc = np.ascontiguousarray(bc, dtype=np.int8)
+        bcp = _p(bc)
+    r = lib().ora_assemble_damage(ctypes.byref(m), _p(lam), _p(mu), _p(u), _p(dnode), bcp, diag, _p(indptr), _p(indices), _p(vals))
+    assert r == 0, r
+    return vals
+
+
+def cell_matrices_elasticity(cell_type, degree, cells, geom, x, lam, mu, qdeg=-1):
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    geom = np.ascontiguousarray(geom, dtype=np.int32)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    nc, nn = cells.shape
+    lam = np.ascontiguousarray(np.broadcast_to(lam, (nc,)), dtype=np.float64)
+    mu = np.ascontiguousarray(np.broadcast_to(mu, (nc,)), dtype=np.float64)
+    nd = nn * _GDIM[cell_type]
+    A = np.zeros((nc, nd, nd))
+    m = _mesh_struct(cell_type, degree, cells, geom, x)
+    r = lib().ora_cell_matrices_elasticity(ctypes.byref(m), _p(lam), _p(mu), qdeg, _p(A))
+    assert r == 0, r
+    return A
+
+
+def e_range(seed: int = 6575) -> np.ndarray:
+    """The reference's 200-entry Young's-modulus table: glibc srand(6575) then
+    E = (1e8-5e6)/199 * (rand() % 200) + 5e6, exactly as
+    FEniCSx/mechanic2d/asym_elasto_damage_model.cc:533-545 and
+    FEniCSx/mechanic2d/asym_elasto_damage_model_symb_sym.py:213-222 compute it (through libc)."""
+    libc = ctypes.CDLL("libc.so.6")
+    libc.srand(seed)
+    a = (1.0e8 - 5.0e6) / 199.0
+    return np.array([a * (libc.rand() % 200) + 5.0e6 for _ in range(200)])
+
+
+def bsr_to_dense(indptr, indices, values, nrows_nodes):
+    bs = values.shape[1]
+    n = nrows_nodes * bs
+    A = np.zeros((n, n))
+    for r in range(nrows_nodes):
+        for s in range(indptr[r], indptr[r + 1]):
+            c = indices[s]
+            A[r * bs:(r + 1) * bs, c * bs:(c + 1) * bs] += values[s]
+    return A

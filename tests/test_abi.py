@@ -1,0 +1,61 @@
+"""CPU checks of the drop-in boundary: libfemasm.so loads and exports every entry point that
+include/femasm.h declares (no compute calls: no GPU here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "femasm.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(fa_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_declares_boundary():
+    names = declared_functions()
+    for n in ["fa_assemble_matrix", "fa_tabulate_cells", "fa_sparsity_count", "fa_sparsity_fill",
+              "fa_build_adjacency", "fa_assemble_vector", "fa_apply_lifting", "fa_set_bc", "fa_last_error"]:
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    from femasm import _lib
+
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libfemasm.so not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    for n in declared_functions():
+        assert hasattr(L, n), n
+    assert set(declared_functions()) == set(_lib.SIGNATURES), "ctypes signature table out of sync with the header"
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    from femasm import _lib
+
+    with pytest.raises(_lib.FemasmError):
+        _lib._lib = None
+        try:
+            _lib.load(str(tmp_path / "nope.so"))
+        finally:
+            _lib._lib = None
+
+
+def test_version_and_element_info():
+    from femasm import _lib
+
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libfemasm.so not built")
+    L = _lib.load()
+    assert L.fa_version() >= 100
+    nn, nq = ctypes.c_int32(), ctypes.c_int32()
+    assert L.fa_element_info(-4, 2, -1, ctypes.byref(nn), ctypes.byref(nq)) == 0
+    assert (nn.value, nq.value) == (10, 4)
+    assert L.fa_element_info(8, 3, -1, ctypes.byref(nn), ctypes.byref(nq)) == 0
+    assert (nn.value, nq.value) == (64, 64)
+    assert L.fa_element_info(-4, 5, -1, ctypes.byref(nn), ctypes.byref(nq)) == -2
+    assert b"unsupported" in L.fa_last_error()
