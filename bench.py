@@ -124,7 +124,8 @@ def main():
     else:
         m, V, a, bcs = build_problem(n, dev)
         A = fem.create_matrix(a)
-        fem.gather_plan(V, A)
+        for part in range(len(A.parts)):
+            fem.gather_plan(V, A, part)
         ncells_local = m.num_cells
 
         def step():

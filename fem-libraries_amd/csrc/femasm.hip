@@ -147,7 +147,9 @@ struct FormView {
 struct BsrView {
   const int64_t* indptr;
   const int32_t* indices;
-  double* data;
+  double* data;        // window base: block indptr[row_begin]
+  int64_t row_begin;   // window [row_begin, row_end)
+  int64_t row_end;
 };
 
 __device__ __forceinline__ void cell_lame(const FormView& F, int64_t c, double& lam, double& mu) {
@@ -433,12 +435,13 @@ __global__ __launch_bounds__(256) void k_cell_blocks(MeshView M, FormView F, Dev
         for (int j = 0; j < GD; ++j) out[(a * GD + i) * nd + b * GD + j] = K[i][j];
     } else {
       int64_t na = M.cells[c * nn + a], nb = M.cells[c * nn + b];
+      if (na < A.row_begin || na >= A.row_end) continue;
       int64_t s = find_slot(A.indptr, A.indices, na, (int32_t)nb);
       if (s < 0) {
         atomicOr(err, 1);
         continue;
       }
-      double* dst = A.data + s * GD * GD;
+      double* dst = A.data + (s - A.indptr[A.row_begin]) * GD * GD;
 #pragma unroll
       for (int i = 0; i < GD; ++i) {
         if (bc && bc[na * GD + i]) continue;
@@ -452,28 +455,52 @@ __global__ __launch_bounds__(256) void k_cell_blocks(MeshView M, FormView F, Dev
   }
 }
 
+// zero the values of the row window (bounds read on the device: no host sync)
+__global__ void k_zero_window(BsrView A, int bs2) {
+  const int64_t n = (A.indptr[A.row_end] - A.indptr[A.row_begin]) * bs2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    A.data[i] = 0.0;
+}
+
 // set bc diagonal entries (after scatter): thread per dof
 template <int GD>
 __global__ void k_bc_diag(BsrView A, int64_t nnodes, const int8_t* __restrict__ bc, double diag, int* err) {
-  int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (n >= nnodes * GD) return;
-  if (!bc[n]) return;
-  int64_t r = n / GD;
-  int i = (int)(n % GD);
-  int64_t s = find_slot(A.indptr, A.indices, r, (int32_t)r);
-  if (s < 0) {
-    atomicOr(err, 2);
-    return;
+  for (int64_t n = A.row_begin * GD + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < A.row_end * GD;
+       n += (int64_t)gridDim.x * blockDim.x) {
+    if (!bc[n]) continue;
+    int64_t r = n / GD;
+    int i = (int)(n % GD);
+    int64_t s = find_slot(A.indptr, A.indices, r, (int32_t)r);
+    if (s < 0) {
+      atomicOr(err, 2);
+      continue;
+    }
+    A.data[(s - A.indptr[A.row_begin]) * GD * GD + i * GD + i] = diag;
   }
-  A.data[s * GD * GD + i * GD + i] = diag;
 }
 
 // ------------------------------------------------------------------------------------ gather kernel
-// LDS budget per workgroup (bytes). Two workgroups of 256 threads per CU fit 160 KiB LDS
-// with room for tables; chunks are planned so that their blocks and adjacency fit.
-static constexpr int kGatherLdsValues = 49152;  // accumulator bytes
-static constexpr int kGatherMaxAdj = 768;       // adjacency entries per chunk
-static constexpr int kGatherMaxRows = 256;      // rows per chunk
+// Two launches per assembly:
+//  1. k_cell_records: one thread per cell packs what every (row, cell) item of the gather
+//     needs into a small record — inverse Jacobian(s), |det J|, lambda, mu (or, for the damage
+//     law, physical gradients, weight and the tangent "hook") — plus a 32-bit mask of the
+//     cell's constrained dofs (bit b*GD+j). A streaming pass: reads the cell's geometry once.
+//  2. k_gather: one workgroup per row chunk (XCD-aware order: chunks of one XCD are
+//     contiguous so its L2 holds the cells they share). Items (adjacency entry, column group)
+//     read one record + the column node ids, build 3x3 blocks in registers and add them into
+//     the LDS copy of the chunk; the chunk is then stored with coalesced plain stores.
+static constexpr int kGatherLdsValues = 32768;  // accumulator bytes per workgroup
+static constexpr int kGatherMaxAdj = 512;       // adjacency entries per chunk
+static constexpr int kGatherMaxRows = 128;      // rows per chunk
+
+template <int GD, int NV, int NQ, int MAT>
+struct Rec {
+  static constexpr bool SIMP = (NV == GD + 1);
+  // LIN simplex: Ji[GD*GD], wdet, lam, mu | LIN tensor: NQ x (Ji[GD*GD], wdet), lam, mu |
+  // DAMAGE (P1 tri): g[3][2], w, H[3][3]
+  static constexpr int RAW = MAT == FA_ASYM_DAMAGE ? 16 : (SIMP ? GD * GD + 3 : NQ * (GD * GD + 1) + 2);
+  static constexpr int SIZE = (RAW + 1) & ~1;  // even: 16-byte aligned records
+};
 
 struct GatherArgs {
   MeshView M;
@@ -482,31 +509,131 @@ struct GatherArgs {
   const int64_t* adj_ptr;
   const int32_t* adj_idx;
   const int64_t* row_start;
+  int64_t nchunks;
   const int8_t* bc;
   double diag;
   const double* tab;  // device tables: wq | dphi | gdphi
-  int nq;
+  const double* rec;  // [ncells][Rec::SIZE]
+  const uint32_t* bcmask;  // [ncells] or NULL
   int* err;
 };
 
+template <int GD, int NN, int NV, int NQ, int MAT>
+__global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, const double* __restrict__ tab,
+                                                      const int8_t* __restrict__ bc, double* __restrict__ rec,
+                                                      uint32_t* __restrict__ bcmask) {
+  using R = Rec<GD, NV, NQ, MAT>;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < M.ncells; c += (int64_t)gridDim.x * blockDim.x) {
+  double r[R::SIZE];
+#pragma unroll
+  for (int k = 0; k < R::SIZE; ++k) r[k] = 0.0;
+  if constexpr (MAT == FA_ASYM_DAMAGE) {
+    double g[3][2], w, H[3][3];
+    damage_cell(M, F, c, g, w, H);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { r[2 * a] = g[a][0]; r[2 * a + 1] = g[a][1]; }
+    r[6] = w;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) r[7 + 3 * i + j] = H[i][j];
+  } else {
+    double lam, mu;
+    cell_lame(F, c, lam, mu);
+    if constexpr (R::SIMP) {
+      double Ji[GD][GD];
+      double det = simplex_geometry<GD>(M, c, Ji);
+#pragma unroll
+      for (int i = 0; i < GD; ++i)
+#pragma unroll
+        for (int k = 0; k < GD; ++k) r[i * GD + k] = Ji[i][k];
+      r[GD * GD] = fabs(det);
+      r[GD * GD + 1] = lam;
+      r[GD * GD + 2] = mu;
+    } else {
+      double xv[NV][GD];
+      const int32_t* gv = M.geom + c * NV;
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int i = 0; i < GD; ++i) xv[v][i] = M.x[(int64_t)gv[v] * GD + i];
+      const double* gdphi = tab + NQ + NQ * NN * GD;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        double Ji[GD][GD];
+        double det = tensor_geometry<GD, NV>(xv, gdphi + q * NV * GD, Ji);
+#pragma unroll
+        for (int i = 0; i < GD; ++i)
+#pragma unroll
+          for (int k = 0; k < GD; ++k) r[q * (GD * GD + 1) + i * GD + k] = Ji[i][k];
+        r[q * (GD * GD + 1) + GD * GD] = fabs(det);
+      }
+      r[NQ * (GD * GD + 1)] = lam;
+      r[NQ * (GD * GD + 1) + 1] = mu;
+    }
+  }
+  double2* out = reinterpret_cast<double2*>(rec + c * R::SIZE);
+#pragma unroll
+  for (int k = 0; k < R::SIZE / 2; ++k) out[k] = make_double2(r[2 * k], r[2 * k + 1]);
+  if (bcmask) {
+    uint32_t m = 0;
+    const int32_t* cn = M.cells + c * NN;
+#pragma unroll
+    for (int b = 0; b < NN; ++b) {
+      int64_t n = cn[b];
+#pragma unroll
+      for (int j = 0; j < GD; ++j) m |= (bc[n * GD + j] ? 1u : 0u) << (b * GD + j);
+    }
+    bcmask[c] = m;
+  }
+  }
+}
+
+// binary search of `col` in cols[lo, hi) (LDS)
+__device__ __forceinline__ int lds_find(const int32_t* cols, int lo, int hi, int32_t col) {
+  int l = lo, h = hi - 1;
+  while (l <= h) {
+    int mid = (l + h) >> 1;
+    int32_t cm = cols[mid];
+    if (cm == col) return mid;
+    if (cm < col) l = mid + 1;
+    else h = mid - 1;
+  }
+  return -1;
+}
+
 // Items are (adjacency entry, column-node group). NSPLIT groups split the cell's NN column
 // nodes so that a chunk exposes enough independent items to all 256 lanes.
+#ifndef FA_GATHER_WAVES
+#define FA_GATHER_WAVES 4  // min waves per SIMD: 4 -> <= 128 VGPRs (16 waves / CU); measured best
+#endif
+#ifndef FA_GATHER_UNROLL_B
+#define FA_GATHER_UNROLL_B 1
+#endif
 template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT>
-__global__ __launch_bounds__(256) void k_gather(GatherArgs P) {
+__global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
+  using R = Rec<GD, NV, NQ, MAT>;
   constexpr int BS2 = GD * GD;
   constexpr int MAXB = kGatherLdsValues / (8 * BS2);
-  constexpr bool SIMP = (NV == GD + 1);
+  constexpr bool SIMP = R::SIMP;
   constexpr int NBG = (NN + NSPLIT - 1) / NSPLIT;  // column nodes per item
   __shared__ double acc[MAXB * BS2];
   __shared__ int32_t cols[MAXB];
   __shared__ int32_t rowoff[kGatherMaxRows + 1];
-  __shared__ uint16_t adjrow[kGatherMaxAdj];
+  __shared__ uint8_t adjrow[kGatherMaxAdj];
   __shared__ double s_w[NQ];
   __shared__ double s_dphi[NQ * NN * GD];
-  __shared__ double s_gdphi[SIMP ? 1 : NQ * NV * GD];
+
+  // XCD-aware chunk order: blocks b and b+8 share an XCD (round-robin dispatch), so XCD
+  // (b % 8) walks the contiguous chunk range [(b % 8) * per, (b % 8 + 1) * per).
+  const int64_t per = (P.nchunks + 7) / 8;
+  for (int64_t vb = blockIdx.x; vb < 8 * per; vb += gridDim.x) {  // gridDim.x % 8 == 0: vb % 8 == blockIdx.x % 8
+  const int64_t chunk = (vb % 8) * per + vb / 8;
+  if (chunk >= P.nchunks) continue;
+  __syncthreads();  // LDS reuse across iterations
 
   const int tid = threadIdx.x;
-  const int64_t r0 = P.row_start[blockIdx.x], r1 = P.row_start[blockIdx.x + 1];
+  const int64_t r0 = P.row_start[chunk], r1 = P.row_start[chunk + 1];
   const int nrows = (int)(r1 - r0);
   const int64_t b0 = P.A.indptr[r0], b1 = P.A.indptr[r1];
   const int nb = (int)(b1 - b0);
@@ -518,12 +645,10 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs P) {
   for (int t = tid; t <= nrows; t += 256) rowoff[t] = (int)(P.A.indptr[r0 + t] - b0);
   for (int t = tid; t < nrows; t += 256) {
     int64_t j0 = P.adj_ptr[r0 + t], j1 = P.adj_ptr[r0 + t + 1];
-    for (int64_t j = j0; j < j1; ++j) adjrow[j - a0] = (uint16_t)t;
+    for (int64_t j = j0; j < j1; ++j) adjrow[j - a0] = (uint8_t)t;
   }
   for (int t = tid; t < NQ; t += 256) s_w[t] = P.tab[t];
   for (int t = tid; t < NQ * NN * GD; t += 256) s_dphi[t] = P.tab[NQ + t];
-  if constexpr (!SIMP)
-    for (int t = tid; t < NQ * NV * GD; t += 256) s_gdphi[t] = P.tab[NQ + NQ * NN * GD + t];
   __syncthreads();
 
   const int nitems = na * NSPLIT;
@@ -534,75 +659,65 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs P) {
     const int aloc = pflat % NN;
     const int lr = adjrow[j];
     const int lo = rowoff[lr], hi = rowoff[lr + 1];
-    const int64_t arow = r0 + lr;
-    const int32_t* cn = P.M.cells + c * NN;
-    bool bca[GD];
+    // one record + the column nodes + the bc mask: all independent loads, issued together
+    double r[R::SIZE];
+    const double2* rp = reinterpret_cast<const double2*>(P.rec + c * R::SIZE);
 #pragma unroll
-    for (int i = 0; i < GD; ++i) bca[i] = P.bc ? (P.bc[arow * GD + i] != 0) : false;
+    for (int k = 0; k < R::SIZE / 2; ++k) {
+      double2 v = rp[k];
+      r[2 * k] = v.x;
+      r[2 * k + 1] = v.y;
+    }
+    int32_t cn[NBG];
+#pragma unroll
+    for (int bb = 0; bb < NBG; ++bb) {
+      const int b = part * NBG + bb;
+      cn[bb] = b < NN ? P.M.cells[c * NN + b] : -1;
+    }
+    const uint32_t mask = P.bcmask ? P.bcmask[c] : 0u;
 
     if constexpr (MAT == FA_ASYM_DAMAGE) {
-      double g[3][2], w, H[3][3];
-      damage_cell(P.M, P.F, c, g, w, H);
-      double ga[2] = {g[aloc][0], g[aloc][1]};
+      double H[3][3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) H[i][k] = r[7 + 3 * i + k];
+      const double w = r[6];
+      double ga[2] = {r[2 * aloc], r[2 * aloc + 1]};
 #pragma unroll
       for (int bb = 0; bb < NBG; ++bb) {
         const int b = part * NBG + bb;
         if (b >= NN) break;
-        double gb[2] = {g[b][0], g[b][1]};
+        double gb[2] = {r[2 * b], r[2 * b + 1]};
         double K[2][2];
         damage_block(ga, gb, w, H, K);
-        const int32_t col = cn[b];
-        int l = lo, h = hi - 1, s = -1;
-        while (l <= h) {
-          int mid = (l + h) >> 1;
-          int32_t cm = cols[mid];
-          if (cm == col) { s = mid; break; }
-          if (cm < col) l = mid + 1; else h = mid - 1;
-        }
+        const int s = lds_find(cols, lo, hi, cn[bb]);
         if (s < 0) { atomicOr(P.err, 1); continue; }
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          if (bca[i]) continue;
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int jj = 0; jj < 2; ++jj) {
-            if (P.bc && P.bc[(int64_t)col * 2 + jj]) continue;
-            atomicAdd(&acc[s * 4 + i * 2 + jj], K[i][jj]);
-          }
-        }
+          for (int jj = 0; jj < 2; ++jj)
+            if (!((mask >> (aloc * 2 + i)) & 1u) && !((mask >> (b * 2 + jj)) & 1u))
+              atomicAdd(&acc[s * 4 + i * 2 + jj], K[i][jj]);
       }
     } else {
-      double lam, mu;
-      cell_lame(P.F, c, lam, mu);
-      // geometry: per-q scaled inverse Jacobians (affine simplex: one)
-      double Ji[SIMP ? 1 : NQ][GD][GD];
-      double wd[NQ];
-      if constexpr (SIMP) {
-        double det = simplex_geometry<GD>(P.M, c, Ji[0]);
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) wd[q] = s_w[q] * fabs(det);
-      } else {
-        double xv[NV][GD];
-        const int32_t* gv = P.M.geom + c * NV;
-#pragma unroll
-        for (int v = 0; v < NV; ++v)
-#pragma unroll
-          for (int i = 0; i < GD; ++i) xv[v][i] = P.M.x[(int64_t)gv[v] * GD + i];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          double det = tensor_geometry<GD, NV>(xv, s_gdphi + q * NV * GD, Ji[q]);
-          wd[q] = s_w[q] * fabs(det);
-        }
-      }
+      const double lam = SIMP ? r[BS2 + 1] : r[NQ * (BS2 + 1)];
+      const double mu = SIMP ? r[BS2 + 2] : r[NQ * (BS2 + 1) + 1];
       // weighted physical gradients of the row node at every quadrature point
       double ga[NQ][GD];
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        double g[GD];
-        phys_grad<GD>(s_dphi + (q * NN + aloc) * GD, Ji[SIMP ? 0 : q], g);
+        const double* Jq = SIMP ? r : r + q * (BS2 + 1);
+        const double wd = s_w[q] * (SIMP ? r[BS2] : Jq[BS2]);
 #pragma unroll
-        for (int d = 0; d < GD; ++d) ga[q][d] = wd[q] * g[d];
+        for (int d = 0; d < GD; ++d) {
+          double sgd = 0.0;
+#pragma unroll
+          for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + aloc) * GD + k] * Jq[k * GD + d];
+          ga[q][d] = wd * sgd;
+        }
       }
-#pragma unroll 2
+#pragma unroll FA_GATHER_UNROLL_B
       for (int bb = 0; bb < NBG; ++bb) {
         const int b = part * NBG + bb;
         if (b >= NN) break;
@@ -613,8 +728,15 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs P) {
           for (int k = 0; k < GD; ++k) G[i][k] = 0.0;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
+          const double* Jq = SIMP ? r : r + q * (BS2 + 1);
           double gb[GD];
-          phys_grad<GD>(s_dphi + (q * NN + b) * GD, Ji[SIMP ? 0 : q], gb);
+#pragma unroll
+          for (int d = 0; d < GD; ++d) {
+            double sgd = 0.0;
+#pragma unroll
+            for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + b) * GD + k] * Jq[k * GD + d];
+            gb[d] = sgd;
+          }
 #pragma unroll
           for (int i = 0; i < GD; ++i)
 #pragma unroll
@@ -622,24 +744,14 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs P) {
         }
         double K[GD][GD];
         lin_block<GD>(G, lam, mu, K);
-        const int32_t col = cn[b];
-        int l = lo, h = hi - 1, s = -1;
-        while (l <= h) {
-          int mid = (l + h) >> 1;
-          int32_t cm = cols[mid];
-          if (cm == col) { s = mid; break; }
-          if (cm < col) l = mid + 1; else h = mid - 1;
-        }
+        const int s = lds_find(cols, lo, hi, cn[bb]);
         if (s < 0) { atomicOr(P.err, 1); continue; }
 #pragma unroll
-        for (int i = 0; i < GD; ++i) {
-          if (bca[i]) continue;
+        for (int i = 0; i < GD; ++i)
 #pragma unroll
-          for (int jj = 0; jj < GD; ++jj) {
-            if (P.bc && P.bc[(int64_t)col * GD + jj]) continue;
-            atomicAdd(&acc[s * BS2 + i * GD + jj], K[i][jj]);
-          }
-        }
+          for (int jj = 0; jj < GD; ++jj)
+            if (!((mask >> (aloc * GD + i)) & 1u) && !((mask >> (b * GD + jj)) & 1u))
+              atomicAdd(&acc[s * BS2 + i * GD + jj], K[i][jj]);
       }
     }
   }
@@ -649,40 +761,38 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs P) {
       const int lr = t / GD, i = t % GD;
       const int64_t r = r0 + lr;
       if (!P.bc[r * GD + i]) continue;
-      int l = rowoff[lr], h = rowoff[lr + 1] - 1, s = -1;
-      while (l <= h) {
-        int mid = (l + h) >> 1;
-        int32_t cm = cols[mid];
-        if (cm == (int32_t)r) { s = mid; break; }
-        if (cm < (int32_t)r) l = mid + 1; else h = mid - 1;
-      }
+      const int s = lds_find(cols, rowoff[lr], rowoff[lr + 1], (int32_t)r);
       if (s < 0) { atomicOr(P.err, 2); continue; }
       acc[s * BS2 + i * GD + i] = P.diag;
     }
     __syncthreads();
   }
-  double* out = P.A.data + b0 * BS2;
+  double* out = P.A.data + (b0 - P.A.indptr[P.A.row_begin]) * BS2;
   for (int t = tid; t < nb * BS2; t += 256) out[t] = acc[t];
+  }
 }
 
 // ------------------------------------------------------------------------------------ adjacency
 __global__ void k_iota(int32_t* v, int64_t n) {
-  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < n) v[i] = (int32_t)i;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    v[i] = (int32_t)i;
 }
 
 __global__ void k_row_ptr_from_sorted(const int32_t* __restrict__ keys, int64_t n, int64_t nnodes, int64_t* __restrict__ ptr) {
-  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i > n) return;
-  int64_t kp = (i == 0) ? -1 : keys[i - 1];
-  int64_t k = (i == n) ? nnodes : keys[i];
-  for (int64_t r = kp + 1; r <= k; ++r) ptr[r] = i;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t kp = (i == 0) ? -1 : keys[i - 1];
+    int64_t k = (i == n) ? nnodes : keys[i];
+    for (int64_t r = kp + 1; r <= k; ++r) ptr[r] = i;
+  }
 }
 
+// AMD dispatches are limited to < 2^32 work-items in total (a larger grid fails silently),
+// so grids are capped and every kernel is written grid-stride.
+static constexpr int64_t kMaxBlocks = (1 << 24) - 8;  // 2^24 x 256 threads < 2^32; multiple of 8
 static int grid_for(int64_t n, int block = 256) {
   int64_t g = (n + block - 1) / block;
   if (g < 1) g = 1;
-  if (g > (1ll << 30)) g = 1ll << 30;
+  if (g > kMaxBlocks) g = kMaxBlocks;
   return (int)g;
 }
 
@@ -737,14 +847,15 @@ __global__ __launch_bounds__(64) void k_sparsity(MeshView M, const int64_t* __re
                                                  const int64_t* __restrict__ indptr, int32_t* __restrict__ indices,
                                                  int* err) {
   __shared__ int32_t s[kSparsityCap];
-  const int64_t r = blockIdx.x;
   const int lane = threadIdx.x;
-  const int64_t j0 = adj_ptr[r], j1 = adj_ptr[r + 1];
   const int nn = M.nn;
+  for (int64_t r = blockIdx.x; r < M.nnodes; r += gridDim.x) {
+  __syncthreads();
+  const int64_t j0 = adj_ptr[r], j1 = adj_ptr[r + 1];
   const int64_t ncand = (j1 - j0) * nn;
   if (ncand > kSparsityCap) {
     if (lane == 0) atomicOr(err, 4);
-    return;
+    continue;
   }
   int n2 = 1;
   while (n2 < ncand) n2 <<= 1;
@@ -786,6 +897,7 @@ __global__ __launch_bounds__(64) void k_sparsity(MeshView M, const int64_t* __re
     running += __popcll(m);
   }
   if (!PASS && lane == 0) counts[r] = running;
+  }
 }
 
 extern "C" int fa_sparsity_count(const fa_mesh* mesh, const fa_adjacency* adj, int64_t* indptr, int64_t* nblocks,
@@ -805,7 +917,7 @@ extern "C" int fa_sparsity_count(const fa_mesh* mesh, const fa_adjacency* adj, i
   HIP_TRY(hipMallocAsync((void**)&counts, sizeof(int64_t) * (n + 1), s));
   HIP_TRY(hipMemsetAsync(counts, 0, sizeof(int64_t) * (n + 1), s));
   if (n > 0) {
-    k_sparsity<0><<<(unsigned)n, 64, 0, s>>>(M, adj->ptr, adj->idx, counts, nullptr, nullptr, derr);
+    k_sparsity<0><<<grid_for(n, 1), 64, 0, s>>>(M, adj->ptr, adj->idx, counts, nullptr, nullptr, derr);
     LAUNCH_CHECK();
   }
   HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, temp_bytes, counts, indptr, (int)(n + 1), s));
@@ -833,7 +945,7 @@ extern "C" int fa_sparsity_fill(const fa_mesh* mesh, const fa_adjacency* adj, co
   HIP_TRY(hipMallocAsync((void**)&derr, sizeof(int), s));
   HIP_TRY(hipMemsetAsync(derr, 0, sizeof(int), s));
   if (mesh->nnodes > 0) {
-    k_sparsity<1><<<(unsigned)mesh->nnodes, 64, 0, s>>>(M, adj->ptr, adj->idx, nullptr, indptr, indices, derr);
+    k_sparsity<1><<<grid_for(mesh->nnodes, 1), 64, 0, s>>>(M, adj->ptr, adj->idx, nullptr, indptr, indices, derr);
     LAUNCH_CHECK();
   }
   int herr = 0;
@@ -851,7 +963,10 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
   if (rc) return rc;
   if (!adj || !A || !row_start || !plan) return fail(FA_E_ARG, "null argument");
   hipStream_t s = (hipStream_t)stream;
-  const int64_t n = mesh->nnodes;
+  int64_t rb0 = A->row_begin, re0 = A->row_end;
+  if (re0 <= rb0) { rb0 = 0; re0 = mesh->nnodes; }
+  if (rb0 < 0 || re0 > mesh->nnodes) return fail(FA_E_ARG, "row window out of range");
+  const int64_t n = re0;
   const int bs2 = mesh->gdim * mesh->gdim;
   const int64_t maxb = kGatherLdsValues / (8 * bs2);
   std::vector<int64_t> ip(n + 1), ap(n + 1);
@@ -859,11 +974,11 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
   HIP_TRY(hipMemcpyAsync(ap.data(), adj->ptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   std::vector<int64_t> rs;
-  rs.reserve(n / 8 + 2);
-  rs.push_back(0);
-  int64_t start = 0;
+  rs.reserve((n - rb0) / 8 + 2);
+  rs.push_back(rb0);
+  int64_t start = rb0;
   int32_t mb = 0, ma = 0;
-  for (int64_t r = 0; r < n; ++r) {
+  for (int64_t r = rb0; r < n; ++r) {
     int64_t rb = ip[r + 1] - ip[r], ra = ap[r + 1] - ap[r];
     if (rb > maxb || ra > kGatherMaxAdj)
       return fail(FA_E_CAPACITY, "row %lld has %lld blocks / %lld cells (gather caps %lld / %d): use FA_SCATTER",
@@ -911,25 +1026,60 @@ static int form_view(const fa_mesh* mesh, const fa_form* form, FormView& F) {
   return FA_OK;
 }
 
-template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT>
-static int launch_gather(const GatherArgs& P, int64_t nchunks, hipStream_t s) {
-  if (nchunks <= 0) return FA_OK;
-  k_gather<GD, NN, NV, NQ, NSPLIT, MAT><<<(unsigned)nchunks, 256, 0, s>>>(P);
-  LAUNCH_CHECK();
+// scratch for per-cell records: stream-ordered, from a pool that keeps its memory
+static int scratch_alloc(void** p, size_t bytes, hipStream_t s) {
+  static bool pool_set = false;
+  if (!pool_set) {
+    int dev = 0;
+    hipMemPool_t pool;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+      uint64_t thr = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+    pool_set = true;
+  }
+  HIP_TRY(hipMallocAsync(p, bytes > 0 ? bytes : 16, s));
   return FA_OK;
 }
 
-static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const GatherArgs& P, int64_t nch, hipStream_t s,
-                           bool* handled) {
+template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT>
+static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s) {
+  using R = Rec<GD, NV, NQ, MAT>;
+  static_assert(NN * GD <= 32, "bc mask holds 32 dofs");
+  const int64_t nc = P.M.ncells;
+  double* rec = nullptr;
+  uint32_t* mask = nullptr;
+  int rc;
+  if ((rc = scratch_alloc((void**)&rec, sizeof(double) * R::SIZE * nc, s))) return rc;
+  if (bc && (rc = scratch_alloc((void**)&mask, sizeof(uint32_t) * nc, s))) return rc;
+  if (nc > 0) {
+    k_cell_records<GD, NN, NV, NQ, MAT><<<grid_for(nc), 256, 0, s>>>(P.M, P.F, P.tab, bc, rec, mask);
+    LAUNCH_CHECK();
+  }
+  P.rec = rec;
+  P.bcmask = mask;
+  if (P.nchunks > 0) {
+    const int64_t per = (P.nchunks + 7) / 8;
+    const int64_t grid = std::min<int64_t>(8 * per, kMaxBlocks);  // kMaxBlocks % 8 == 0
+    k_gather<GD, NN, NV, NQ, NSPLIT, MAT><<<(unsigned)grid, 256, 0, s>>>(P);
+    LAUNCH_CHECK();
+  }
+  HIP_TRY(hipFreeAsync(rec, s));
+  if (mask) HIP_TRY(hipFreeAsync(mask, s));
+  return FA_OK;
+}
+
+static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const GatherArgs& P, const int8_t* bc,
+                           hipStream_t s, bool* handled) {
   *handled = true;
   const int ct = m->cell_type, p = m->degree, nq = T.nq;
-  if (kind == FA_ASYM_DAMAGE) return launch_gather<2, 3, 3, 1, 1, FA_ASYM_DAMAGE>(P, nch, s);
-  if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, 0>(P, nch, s);
-  if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, 0>(P, nch, s);
-  if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, 0>(P, nch, s);
-  if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, 2, 0>(P, nch, s);
-  if (ct == FA_QUADRILATERAL && p == 1 && nq == 4) return launch_gather<2, 4, 4, 4, 1, 0>(P, nch, s);
-  if (ct == FA_QUADRILATERAL && p == 2 && nq == 9) return launch_gather<2, 9, 4, 9, 3, 0>(P, nch, s);
+  if (kind == FA_ASYM_DAMAGE) return launch_gather<2, 3, 3, 1, 1, FA_ASYM_DAMAGE>(P, bc, s);
+  if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, 0>(P, bc, s);
+  if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, 0>(P, bc, s);
+  if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, 0>(P, bc, s);
+  if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, 2, 0>(P, bc, s);
+  if (ct == FA_QUADRILATERAL && p == 1 && nq == 4) return launch_gather<2, 4, 4, 4, 1, 0>(P, bc, s);
+  if (ct == FA_QUADRILATERAL && p == 2 && nq == 9) return launch_gather<2, 9, 4, 9, 3, 0>(P, bc, s);
   *handled = false;
   return FA_OK;
 }
@@ -968,7 +1118,7 @@ extern "C" int fa_tabulate_cells(const fa_mesh* mesh, const fa_form* form, int64
   DevTables T;
   if ((rc = get_tables(mesh->cell_type, mesh->degree, form->qdeg, &T))) return rc;
   MeshView M{mesh->cells, mesh->geom, mesh->x, mesh->ncells, mesh->nnodes, mesh->nn, mesh->nv, mesh->gdim};
-  BsrView A{nullptr, nullptr, nullptr};
+  BsrView A{nullptr, nullptr, nullptr, 0, 0};
   return launch_cell_blocks(0, mesh, M, F, T, c0, ncells_out, Ae, A, nullptr, nullptr, (hipStream_t)stream);
 }
 
@@ -980,13 +1130,16 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
   if (rc) return rc;
   if (!A || !A->indptr || !A->indices || !A->data) return fail(FA_E_ARG, "null matrix");
   if (A->bs != mesh->gdim || A->nrows != mesh->nnodes) return fail(FA_E_ARG, "matrix shape does not match mesh");
+  int64_t wb = A->row_begin, we = A->row_end;
+  if (we <= wb) { wb = 0; we = mesh->nnodes; }
+  if (wb < 0 || we > mesh->nnodes) return fail(FA_E_ARG, "row window out of range");
   FormView F;
   if ((rc = form_view(mesh, form, F))) return rc;
   DevTables T;
   if ((rc = get_tables(mesh->cell_type, mesh->degree, form->qdeg, &T))) return rc;
   hipStream_t s = (hipStream_t)stream;
   MeshView M{mesh->cells, mesh->geom, mesh->x, mesh->ncells, mesh->nnodes, mesh->nn, mesh->nv, mesh->gdim};
-  BsrView Av{A->indptr, A->indices, A->data};
+  BsrView Av{A->indptr, A->indices, A->data, wb, we};
   static int* derr = nullptr;  // per-process device error word (sticky until read)
   if (!derr) {
     HIP_TRY(hipMalloc((void**)&derr, sizeof(int)));
@@ -998,10 +1151,10 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
       return fail(FA_E_ARG, "FA_GATHER needs the adjacency and a plan (fa_plan_gather)");
     GatherArgs P;
     P.M = M; P.F = F; P.A = Av;
-    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start;
-    P.bc = bc; P.diag = diag; P.tab = T.wq; P.nq = T.nq; P.err = derr;
+    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks;
+    P.bc = bc; P.diag = diag; P.tab = T.wq; P.rec = nullptr; P.bcmask = nullptr; P.err = derr;
     bool handled = false;
-    rc = dispatch_gather(mesh, T, F.kind, P, plan->nchunks, s, &handled);
+    rc = dispatch_gather(mesh, T, F.kind, P, bc, s, &handled);
     if (rc) return rc;
     if (!handled) scatter = true;  // no specialised gather kernel: generic element scatter
   }
@@ -1009,11 +1162,14 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     // the generic fallback of FA_GATHER writes every value, so it starts from zero;
     // FA_SCATTER accumulates into A unless FA_ZERO_FIRST (MatZeroEntries) is set
     if (!(flags & FA_SCATTER) || (flags & FA_ZERO_FIRST))
-      HIP_TRY(hipMemsetAsync(A->data, 0, sizeof(double) * A->nblocks * A->bs * A->bs, s));
+    {
+      k_zero_window<<<4096, 256, 0, s>>>(Av, A->bs * A->bs);
+      LAUNCH_CHECK();
+    }
     rc = launch_cell_blocks(1, mesh, M, F, T, 0, mesh->ncells, nullptr, Av, bc, derr, s);
     if (rc) return rc;
     if (bc) {
-      int64_t n = mesh->nnodes * mesh->gdim;
+      int64_t n = (we - wb) * mesh->gdim;
       if (mesh->gdim == 2) k_bc_diag<2><<<grid_for(n), 256, 0, s>>>(Av, mesh->nnodes, bc, diag, derr);
       else k_bc_diag<3><<<grid_for(n), 256, 0, s>>>(Av, mesh->nnodes, bc, diag, derr);
       LAUNCH_CHECK();
@@ -1045,9 +1201,8 @@ extern "C" int fa_apply_lifting(const fa_mesh* mesh, const fa_form* form, double
 
 __global__ void k_set_bc(double* __restrict__ b, int64_t n, const int8_t* __restrict__ bc, const double* __restrict__ g,
                          const double* __restrict__ x0, double alpha) {
-  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= n || !bc[i]) return;
-  b[i] = alpha * (g[i] - (x0 ? x0[i] : 0.0));
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (bc[i]) b[i] = alpha * (g[i] - (x0 ? x0[i] : 0.0));
 }
 
 extern "C" int fa_set_bc(double* b, int64_t ndofs, const int8_t* bc, const double* g, const double* x0, double alpha,

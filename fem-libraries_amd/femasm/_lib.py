@@ -62,6 +62,8 @@ class fa_bsr(ctypes.Structure):
         ("indptr", ctypes.c_void_p),
         ("indices", ctypes.c_void_p),
         ("data", ctypes.c_void_p),
+        ("row_begin", ctypes.c_int64),
+        ("row_end", ctypes.c_int64),
     ]
 
 
@@ -104,7 +106,7 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or LIB_PATH
+    path = path or os.environ.get("FEMASM_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise FemasmError(
             f"{path} is missing: build it with `make -C {CSRC}` (hipcc --offload-arch=gfx950) "

@@ -413,7 +413,7 @@ def _fa_form(a) -> _lib.fa_form:
     return f
 
 
-def create_matrix(a) -> MatrixCSR:
+def create_matrix(a, max_part_bytes: int | None = None) -> MatrixCSR:
     """Sparsity pattern of the bilinear form (all node pairs of every cell), built on the GPU
     (dolfinx.fem.petsc.create_matrix, FEniCSx/mechanic2d/asym_elasto_damage_model.cc:688)."""
     V = a.V
@@ -432,35 +432,40 @@ def create_matrix(a) -> MatrixCSR:
                    "fa_sparsity_fill")
         V._pattern = (indptr, indices)
     indptr, indices = V._pattern
-    return MatrixCSR(indptr, indices, V.bs)
+    if max_part_bytes is None:
+        return MatrixCSR(indptr, indices, V.bs)
+    return MatrixCSR(indptr, indices, V.bs, max_part_bytes=max_part_bytes)
 
 
-def _fa_bsr(A: MatrixCSR) -> _lib.fa_bsr:
+def _fa_bsr(A: MatrixCSR, part: int = 0) -> _lib.fa_bsr:
+    r0, r1, data = A.parts[part]
     b = _lib.fa_bsr()
     b.nrows = A.num_block_rows
     b.bs = A.bs
     b.nblocks = A.num_blocks
     b.indptr = A.indptr.data_ptr()
     b.indices = A.indices.data_ptr()
-    b.data = A.data.data_ptr()
+    b.data = data.data_ptr()
+    b.row_begin = r0
+    b.row_end = r1
     return b
 
 
-def gather_plan(V: FunctionSpace, A: MatrixCSR):
-    """Row-chunk plan of the gather kernel for A's pattern (cached on the matrix)."""
-    plan = V.__dict__.get("_plan")
-    if plan is None or plan[2] is not A.indptr:
+def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0):
+    """Row-chunk plan of the gather kernel for one row part of A's pattern (cached on V)."""
+    plans = V.__dict__.setdefault("_plans", {})
+    key = (A.indptr.data_ptr(), A.parts[part][0], A.parts[part][1])
+    if key not in plans:
         L = _lib.load()
         fm = V._fa_mesh()
         adj = V._fa_adjacency()
-        fb = _fa_bsr(A)
-        rs = torch.empty(V.num_nodes + 1, dtype=torch.int64, device=V.mesh.device)
+        fb = _fa_bsr(A, part)
+        rs = torch.empty(A.parts[part][1] - A.parts[part][0] + 1, dtype=torch.int64, device=V.mesh.device)
         plan = _lib.fa_plan()
         _lib.check(L.fa_plan_gather(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), rs.data_ptr(),
                                     ctypes.byref(plan), _lib.stream_handle(V.mesh.device)), "fa_plan_gather")
-        V._plan = (plan, rs, A.indptr)
-        plan = V._plan
-    return plan[0]
+        plans[key] = (plan, rs, A.indptr)
+    return plans[key][0]
 
 
 def assemble_matrix(a, bcs=None, diagonal: float = 1.0, A: MatrixCSR | None = None, method: str = "gather") -> MatrixCSR:
@@ -477,19 +482,20 @@ def assemble_matrix(a, bcs=None, diagonal: float = 1.0, A: MatrixCSR | None = No
     marker, _ = _combine_bcs(V, bcs)
     fm = V._fa_mesh()
     ff = _fa_form(a)
-    fb = _fa_bsr(A)
     sh = _lib.stream_handle(V.mesh.device)
-    if method == "gather":
-        adj = V._fa_adjacency()
-        plan = gather_plan(V, A)
-        rc = L.fa_assemble_matrix(ctypes.byref(fm), ctypes.byref(ff), ctypes.byref(adj), ctypes.byref(plan),
-                                  _lib.ptr(marker), float(diagonal), ctypes.byref(fb), _lib.FA_GATHER, sh)
-    elif method == "scatter":
-        rc = L.fa_assemble_matrix(ctypes.byref(fm), ctypes.byref(ff), None, None, _lib.ptr(marker), float(diagonal),
-                                  ctypes.byref(fb), _lib.FA_SCATTER | _lib.FA_ZERO_FIRST, sh)
-    else:
-        raise ValueError(f"unknown method {method}")
-    _lib.check(rc, "fa_assemble_matrix")
+    for part in range(len(A.parts)):
+        fb = _fa_bsr(A, part)
+        if method == "gather":
+            adj = V._fa_adjacency()
+            plan = gather_plan(V, A, part)
+            rc = L.fa_assemble_matrix(ctypes.byref(fm), ctypes.byref(ff), ctypes.byref(adj), ctypes.byref(plan),
+                                      _lib.ptr(marker), float(diagonal), ctypes.byref(fb), _lib.FA_GATHER, sh)
+        elif method == "scatter":
+            rc = L.fa_assemble_matrix(ctypes.byref(fm), ctypes.byref(ff), None, None, _lib.ptr(marker),
+                                      float(diagonal), ctypes.byref(fb), _lib.FA_SCATTER | _lib.FA_ZERO_FIRST, sh)
+        else:
+            raise ValueError(f"unknown method {method}")
+        _lib.check(rc, "fa_assemble_matrix")
     A._keepalive = (marker, a)
     return A
 

@@ -11,14 +11,48 @@ import numpy as np
 import torch
 
 
+# Largest single values allocation; larger matrices are split into row parts (each assembled
+# through the fa_bsr row window). Config E (138 GB) fits one part on a 288 GB MI355X.
+import os
+
+MAX_PART_BYTES = int(float(os.environ.get("FEMASM_MAX_PART_GB", "200")) * (1 << 30))
+
+
 class MatrixCSR:
-    def __init__(self, indptr: torch.Tensor, indices: torch.Tensor, bs: int, data: torch.Tensor | None = None):
+    """Block-CSR matrix; values may be split into row parts (each its own allocation).
+
+    ``parts``: list of (row_begin, row_end, data[indptr[row_end]-indptr[row_begin], bs, bs]).
+    """
+
+    def __init__(self, indptr: torch.Tensor, indices: torch.Tensor, bs: int, data: torch.Tensor | None = None,
+                 max_part_bytes: int = MAX_PART_BYTES):
         self.indptr = indptr
         self.indices = indices
         self.bs = int(bs)
-        if data is None:
-            data = torch.zeros((indices.shape[0], bs, bs), dtype=torch.float64, device=indices.device)
-        self.data = data
+        nrows = int(indptr.shape[0] - 1)
+        if data is not None:
+            self.parts = [(0, nrows, data)]
+            return
+        block_bytes = 8 * self.bs * self.bs
+        nb = int(indices.shape[0])
+        cap = max(1, max_part_bytes // block_bytes)
+        bounds = [0]
+        if nb > cap:
+            targets = torch.arange(cap, nb, cap, device=indptr.device, dtype=torch.int64)
+            cuts = torch.searchsorted(indptr, targets, right=True) - 1
+            bounds += sorted({int(c) for c in cuts.cpu().tolist() if 0 < int(c) < nrows})
+        bounds.append(nrows)
+        self.parts = []
+        for r0, r1 in zip(bounds[:-1], bounds[1:]):
+            n = int(indptr[r1]) - int(indptr[r0])
+            self.parts.append((r0, r1, torch.zeros((n, self.bs, self.bs), dtype=torch.float64, device=indices.device)))
+
+    @property
+    def data(self) -> torch.Tensor:
+        """All values [nblocks, bs, bs] (a concatenated copy when the matrix has several parts)."""
+        if len(self.parts) == 1:
+            return self.parts[0][2]
+        return torch.cat([p[2] for p in self.parts])
 
     @property
     def num_block_rows(self) -> int:
@@ -38,7 +72,8 @@ class MatrixCSR:
         return self.num_blocks * self.bs * self.bs
 
     def zero(self):
-        self.data.zero_()
+        for _, _, d in self.parts:
+            d.zero_()
 
     def to_scipy(self):
         """scipy.sparse.bsr_matrix on the host (test / debug helper)."""
@@ -50,6 +85,21 @@ class MatrixCSR:
 
     def to_dense(self) -> np.ndarray:
         return self.to_scipy().toarray()
+
+    def row_blocks(self, rows) -> tuple[list, list]:
+        """Column indices and value blocks of the given block rows (host numpy), across parts."""
+        ip = self.indptr
+        out_c, out_v = [], []
+        for r in rows:
+            r = int(r)
+            for r0, r1, d in self.parts:
+                if r0 <= r < r1:
+                    b, e = int(ip[r]), int(ip[r + 1])
+                    base = int(ip[r0])
+                    out_c.append(self.indices[b:e].cpu().numpy())
+                    out_v.append(d[b - base:e - base].cpu().numpy())
+                    break
+        return out_c, out_v
 
     def diagonal_block_slots(self) -> torch.Tensor:
         """Slot index of the diagonal block of every row (-1 if absent)."""

@@ -94,8 +94,12 @@ typedef struct {
   int64_t nblocks;       /* indices length */
   const int64_t* indptr; /* [nrows+1] */
   const int32_t* indices;/* [nblocks], sorted per row */
-  double* data;          /* [nblocks][bs][bs] row-major blocks */
+  double* data;          /* blocks of rows [row_begin, row_end): [indptr[row_end]-indptr[row_begin]][bs][bs] */
+  int64_t row_begin;     /* row window held by `data` (a row part of the matrix, or the rows a rank */
+  int64_t row_end;       /* owns); row_end <= row_begin means the whole matrix [0, nrows) */
 } fa_bsr;
+/* A row window lets a caller hold the values of a row range only: a rank's owned rows, or a
+ * matrix split into several allocations (femasm.la.MatrixCSR parts). */
 
 typedef struct {
   const int64_t* ptr;    /* [nnodes+1] */

@@ -217,3 +217,20 @@ def test_gather_equals_scatter_larger(oracle, dev):
     # gather is run-to-run reproducible
     A3 = fem.assemble_matrix(a, method="gather")
     assert ((A3.data - d1).abs().max() <= 1e-15 * scale).item()
+
+
+@pytest.mark.parametrize("method", ["gather", "scatter"])
+@pytest.mark.parametrize("ct,p,n", [(-4, 2, (3, 3, 2)), (3, 1, (9, 6)), (8, 2, (2, 2, 2))])
+def test_row_parts(oracle, dev, ct, p, n, method):
+    """Values split into many row parts (each its own allocation, row window in fa_bsr)."""
+    from femasm import fem
+
+    m, V, a = _setup(oracle, ct, p, n, dev)
+    left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
+    bcs = [fem.dirichletbc(0.0, left, V)]
+    A = fem.create_matrix(a, max_part_bytes=4096)
+    assert len(A.parts) > 3
+    fem.assemble_matrix(a, bcs=bcs, A=A, method=method)
+    marker, _ = fem._combine_bcs(V, bcs)
+    _, _, ref = _oracle_matrix(oracle, V, a, marker=marker)
+    _assert_close(A, ref)
