@@ -71,6 +71,7 @@ struct DevTables {
   const double* gdphi;
   const double* phi;
   const double* gphi;
+  const double* ahat;  // simplex only: [nn][nn][td][td] = sum_q w_q dphi_a(q) dphi_b(q)^T
   int ndoubles;
 };
 
@@ -98,6 +99,19 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
   h.insert(h.end(), T.gdphi.begin(), T.gdphi.end());
   h.insert(h.end(), T.phi.begin(), T.phi.end());
   h.insert(h.end(), T.gphi.begin(), T.gphi.end());
+  // reference tensor of grad-grad products (affine simplices: G_ab = |J| Ji^T Ahat_ab Ji)
+  const size_t off_ahat = h.size();
+  if (is_simplex(ct)) {
+    for (int a = 0; a < T.nn; ++a)
+      for (int b = 0; b < T.nn; ++b)
+        for (int i = 0; i < T.td; ++i)
+          for (int j = 0; j < T.td; ++j) {
+            double v = 0.0;
+            for (int q = 0; q < T.nq; ++q)
+              v += T.wq[q] * T.dphi[((size_t)q * T.nn + a) * T.td + i] * T.dphi[((size_t)q * T.nn + b) * T.td + j];
+            h.push_back(v);
+          }
+  }
   double* d = nullptr;
   HIP_TRY(hipMalloc(&d, h.size() * sizeof(double)));
   HIP_TRY(hipMemcpy(d, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -108,6 +122,7 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
   D.gdphi = D.dphi + (size_t)T.nq * T.nn * T.td;
   D.phi = D.gdphi + (size_t)T.nq * T.nv * T.td;
   D.gphi = D.phi + (size_t)T.nq * T.nn;
+  D.ahat = is_simplex(ct) ? d + off_ahat : nullptr;
   D.ndoubles = (int)h.size();
   g_tabs[key] = D;
   *out = D;
@@ -489,7 +504,10 @@ __global__ void k_bc_diag(BsrView A, int64_t nnodes, const int8_t* __restrict__ 
 //     contiguous so its L2 holds the cells they share). Items (adjacency entry, column group)
 //     read one record + the column node ids, build 3x3 blocks in registers and add them into
 //     the LDS copy of the chunk; the chunk is then stored with coalesced plain stores.
-static constexpr int kGatherLdsValues = 32768;  // accumulator bytes per workgroup
+#ifndef FA_GATHER_LDS
+#define FA_GATHER_LDS 28672
+#endif
+static constexpr int kGatherLdsValues = FA_GATHER_LDS;  // accumulator bytes per workgroup (4 WG / CU)
 static constexpr int kGatherMaxAdj = 512;       // adjacency entries per chunk
 static constexpr int kGatherMaxRows = 128;      // rows per chunk
 
@@ -513,6 +531,7 @@ struct GatherArgs {
   const int8_t* bc;
   double diag;
   const double* tab;  // device tables: wq | dphi | gdphi
+  const double* ahat; // simplex reference tensor [nn][nn][GD][GD]
   const double* rec;  // [ncells][Rec::SIZE]
   const uint32_t* bcmask;  // [ncells] or NULL
   int* err;
@@ -621,8 +640,9 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   __shared__ int32_t cols[MAXB];
   __shared__ int32_t rowoff[kGatherMaxRows + 1];
   __shared__ uint8_t adjrow[kGatherMaxAdj];
-  __shared__ double s_w[NQ];
-  __shared__ double s_dphi[NQ * NN * GD];
+  __shared__ double s_w[SIMP ? 1 : NQ];
+  __shared__ double s_dphi[SIMP ? 1 : NQ * NN * GD];
+  __shared__ double s_ahat[SIMP ? NN * NN * BS2 : 1];
 
   // XCD-aware chunk order: blocks b and b+8 share an XCD (round-robin dispatch), so XCD
   // (b % 8) walks the contiguous chunk range [(b % 8) * per, (b % 8 + 1) * per).
@@ -647,8 +667,12 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     int64_t j0 = P.adj_ptr[r0 + t], j1 = P.adj_ptr[r0 + t + 1];
     for (int64_t j = j0; j < j1; ++j) adjrow[j - a0] = (uint8_t)t;
   }
-  for (int t = tid; t < NQ; t += 256) s_w[t] = P.tab[t];
-  for (int t = tid; t < NQ * NN * GD; t += 256) s_dphi[t] = P.tab[NQ + t];
+  if constexpr (SIMP) {
+    for (int t = tid; t < NN * NN * BS2; t += 256) s_ahat[t] = P.ahat[t];
+  } else {
+    for (int t = tid; t < NQ; t += 256) s_w[t] = P.tab[t];
+    for (int t = tid; t < NQ * NN * GD; t += 256) s_dphi[t] = P.tab[NQ + t];
+  }
   __syncthreads();
 
   const int nitems = na * NSPLIT;
@@ -700,15 +724,54 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
             if (!((mask >> (aloc * 2 + i)) & 1u) && !((mask >> (b * 2 + jj)) & 1u))
               atomicAdd(&acc[s * 4 + i * 2 + jj], K[i][jj]);
       }
+    } else if constexpr (SIMP) {
+      // affine simplex: G_ab = |J| Ji^T Ahat_ab Ji  (reference-tensor form)
+      const double wdet = r[BS2], lam = r[BS2 + 1] * wdet, mu = r[BS2 + 2] * wdet;
+#pragma unroll FA_GATHER_UNROLL_B
+      for (int bb = 0; bb < NBG; ++bb) {
+        const int b = part * NBG + bb;
+        if (b >= NN) break;
+        const double* Ah = s_ahat + (aloc * NN + b) * BS2;
+        double T[GD][GD];  // T = Ahat Ji
+#pragma unroll
+        for (int i = 0; i < GD; ++i)
+#pragma unroll
+          for (int d = 0; d < GD; ++d) {
+            double t = 0.0;
+#pragma unroll
+            for (int k = 0; k < GD; ++k) t += Ah[i * GD + k] * r[k * GD + d];
+            T[i][d] = t;
+          }
+        double G[GD][GD];  // G = Ji^T T
+#pragma unroll
+        for (int e = 0; e < GD; ++e)
+#pragma unroll
+          for (int d = 0; d < GD; ++d) {
+            double g = 0.0;
+#pragma unroll
+            for (int i = 0; i < GD; ++i) g += r[i * GD + e] * T[i][d];
+            G[e][d] = g;
+          }
+        double K[GD][GD];
+        lin_block<GD>(G, lam, mu, K);
+        const int s = lds_find(cols, lo, hi, cn[bb]);
+        if (s < 0) { atomicOr(P.err, 1); continue; }
+#pragma unroll
+        for (int i = 0; i < GD; ++i)
+#pragma unroll
+          for (int jj = 0; jj < GD; ++jj)
+            if (!((mask >> (aloc * GD + i)) & 1u) && !((mask >> (b * GD + jj)) & 1u))
+              atomicAdd(&acc[s * BS2 + i * GD + jj], K[i][jj]);
+      }
     } else {
-      const double lam = SIMP ? r[BS2 + 1] : r[NQ * (BS2 + 1)];
-      const double mu = SIMP ? r[BS2 + 2] : r[NQ * (BS2 + 1) + 1];
+      const double lam = r[NQ * (BS2 + 1)];
+      const double mu = r[NQ * (BS2 + 1) + 1];
       // weighted physical gradients of the row node at every quadrature point
       double ga[NQ][GD];
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        const double* Jq = SIMP ? r : r + q * (BS2 + 1);
-        const double wd = s_w[q] * (SIMP ? r[BS2] : Jq[BS2]);
+        const double* Jq = r + q * (BS2 + 1);
+        const double wd = s_w[q] * Jq[BS2];
 #pragma unroll
         for (int d = 0; d < GD; ++d) {
           double sgd = 0.0;
@@ -728,7 +791,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
           for (int k = 0; k < GD; ++k) G[i][k] = 0.0;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-          const double* Jq = SIMP ? r : r + q * (BS2 + 1);
+          const double* Jq = r + q * (BS2 + 1);
           double gb[GD];
 #pragma unroll
           for (int d = 0; d < GD; ++d) {
@@ -1069,6 +1132,9 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s) {
   return FA_OK;
 }
 
+#ifndef FA_P2TET_NSPLIT
+#define FA_P2TET_NSPLIT 2  // measured best with the reference-tensor blocks (n=120 sweep)
+#endif
 static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const GatherArgs& P, const int8_t* bc,
                            hipStream_t s, bool* handled) {
   *handled = true;
@@ -1077,7 +1143,7 @@ static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const
   if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, 0>(P, bc, s);
   if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, 0>(P, bc, s);
   if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, 0>(P, bc, s);
-  if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, 2, 0>(P, bc, s);
+  if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, FA_P2TET_NSPLIT, 0>(P, bc, s);
   if (ct == FA_QUADRILATERAL && p == 1 && nq == 4) return launch_gather<2, 4, 4, 4, 1, 0>(P, bc, s);
   if (ct == FA_QUADRILATERAL && p == 2 && nq == 9) return launch_gather<2, 9, 4, 9, 3, 0>(P, bc, s);
   *handled = false;
@@ -1152,7 +1218,7 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     GatherArgs P;
     P.M = M; P.F = F; P.A = Av;
     P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks;
-    P.bc = bc; P.diag = diag; P.tab = T.wq; P.rec = nullptr; P.bcmask = nullptr; P.err = derr;
+    P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr;
     bool handled = false;
     rc = dispatch_gather(mesh, T, F.kind, P, bc, s, &handled);
     if (rc) return rc;
