@@ -42,7 +42,7 @@ def is_simplex(ct) -> bool:
     return CellType(ct) in (CellType.triangle, CellType.tetrahedron)
 
 
-def num_nodes(ct, p: int) -> int:
+def num_nodes_of(ct, p: int) -> int:
     ct = CellType(ct)
     return {CellType.triangle: (p + 1) * (p + 2) // 2, CellType.tetrahedron: (p + 1) * (p + 2) * (p + 3) // 6,
             CellType.quadrilateral: (p + 1) ** 2, CellType.hexahedron: (p + 1) ** 3}[ct]
@@ -122,7 +122,7 @@ class FunctionSpace:
             return
         if family not in ("Lagrange", "P", "Q", "CG"):
             raise ValueError(f"unsupported family {family}")
-        self.nn = num_nodes(mesh.cell_type, self.degree)
+        self.nn = num_nodes_of(mesh.cell_type, self.degree)
         if self.degree == 1:
             self.dofmap = mesh.cells
             self.num_nodes = mesh.num_vertices
@@ -131,6 +131,18 @@ class FunctionSpace:
         else:
             self.dofmap, self.num_nodes = _generic_dofmap(mesh, self.degree)
         self._x = None
+
+    @classmethod
+    def from_dofmap(cls, mesh: Mesh, degree: int, bs: int, dofmap: torch.Tensor, num_nodes: int) -> "FunctionSpace":
+        """A Lagrange space with a caller-supplied node numbering (e.g. a rank-local numbering
+        of a slab of a larger mesh: femasm.parallel)."""
+        V = cls.__new__(cls)
+        V.mesh, V.family, V.degree, V.bs = mesh, "Lagrange", int(degree), int(bs)
+        V.nn = num_nodes_of(mesh.cell_type, int(degree))
+        V.dofmap = dofmap.to(torch.int32).contiguous()
+        V.num_nodes = int(num_nodes)
+        V._adjacency, V._pattern, V._x = None, None, None
+        return V
 
     @property
     def num_dofs(self) -> int:

@@ -25,13 +25,18 @@ class MatrixCSR:
     """
 
     def __init__(self, indptr: torch.Tensor, indices: torch.Tensor, bs: int, data: torch.Tensor | None = None,
-                 max_part_bytes: int = MAX_PART_BYTES):
+                 max_part_bytes: int = MAX_PART_BYTES, window: tuple | None = None):
         self.indptr = indptr
         self.indices = indices
         self.bs = int(bs)
         nrows = int(indptr.shape[0] - 1)
         if data is not None:
             self.parts = [(0, nrows, data)]
+            return
+        if window is not None:  # only rows [r0, r1) are held (a rank's rows)
+            r0, r1 = int(window[0]), int(window[1])
+            n = int(indptr[r1]) - int(indptr[r0])
+            self.parts = [(r0, r1, torch.zeros((n, self.bs, self.bs), dtype=torch.float64, device=indices.device))]
             return
         block_bytes = 8 * self.bs * self.bs
         nb = int(indices.shape[0])

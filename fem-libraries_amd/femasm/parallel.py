@@ -1,0 +1,183 @@
+"""Multi-GPU assembly: z-slab sharding of a structured box with an RCCL boundary exchange.
+
+The reference runs one MPI rank per core on a (Par)METIS partition and sums the contributions
+to rows owned by another rank inside PETSc's ``MatAssemblyBegin/End`` stash
+(FEniCSx/mechanic2d/asym_elasto_damage_model.cc:853-859; MFEM: hypre PtAP). Here one process per
+GPU owns a slab of cube layers [k0, k1) of an n_x x n_y x n_z box:
+
+* its cells are the cells of its own layers (assembled with the gather kernel);
+* its sparsity pattern comes from its layers plus one ghost layer on each side, so the rows of
+  the two interface planes (z = k0 and z = k1) carry the full global pattern on both neighbours;
+* rows are the lattice planes p*k0 .. p*k1 of the degree-p lattice (a fa_bsr row window); with
+  lattice numbering each interface plane is one contiguous slab of BSR values;
+* the only exchange is, per slab boundary, ONE all-reduce(SUM) of that slab between the two
+  neighbouring ranks (a 2-rank process group: xGMI is point-to-point, a global all-reduce of all
+  interfaces would be link-bound — SURVEY.md §5). Boundaries are processed in two phases (even
+  pairs, then odd pairs) so the collectives of every rank are issued in a compatible order.
+* interface rows are owned by the lower rank (doc.tex:464); after the sum both copies are equal,
+  and Dirichlet diagonals on interface rows (inserted by both ranks) are reset to `diagonal`.
+
+The partition / numbering logic (``SlabPartition``) and the exchange (``exchange_interfaces``) are
+device-agnostic (torch tensors on any device, any torch.distributed backend: tested with gloo on
+CPU, run with nccl = RCCL on MI355X).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+
+def slab_layers(nz: int, world: int, rank: int) -> tuple[int, int]:
+    """Balanced split of nz cube layers over `world` ranks: rank gets [k0, k1)."""
+    base, extra = divmod(nz, world)
+    k0 = rank * base + min(rank, extra)
+    return k0, k0 + base + (1 if rank < extra else 0)
+
+
+@dataclass
+class SlabPartition:
+    n: tuple  # cubes per direction (nx, ny, nz)
+    degree: int
+    rank: int
+    world: int
+
+    def __post_init__(self):
+        nx, ny, nz = self.n
+        p = self.degree
+        if nz < self.world:
+            raise ValueError(f"{nz} layers cannot be split over {self.world} ranks")
+        self.k0, self.k1 = slab_layers(nz, self.world, self.rank)
+        self.kp0, self.kp1 = max(self.k0 - 1, 0), min(self.k1 + 1, nz)  # pattern layers (with ghosts)
+        self.plane = (p * nx + 1) * (p * ny + 1)  # nodes per lattice plane
+        self.node_offset = p * self.kp0 * self.plane  # local node = global node - node_offset
+        self.num_local_nodes = self.plane * (p * (self.kp1 - self.kp0) + 1)
+        # row window: lattice planes p*k0 .. p*k1 (inclusive), in local numbering
+        self.row_begin = p * (self.k0 - self.kp0) * self.plane
+        self.row_end = (p * (self.k1 - self.kp0) + 1) * self.plane
+        self.lower = None if self.rank == 0 else (self.row_begin, self.row_begin + self.plane)
+        self.upper = None if self.rank == self.world - 1 else (self.row_end - self.plane, self.row_end)
+
+    @property
+    def owned_rows(self) -> tuple[int, int]:
+        """Rows this rank owns (interface planes belong to the lower rank)."""
+        return (self.row_begin + (self.plane if self.rank > 0 else 0), self.row_end)
+
+    def to_local(self, global_nodes: torch.Tensor) -> torch.Tensor:
+        return (global_nodes.to(torch.int64) - self.node_offset).to(torch.int32)
+
+
+def make_pair_groups(world: int):
+    """One 2-rank group per slab boundary (created collectively, same order on every rank)."""
+    import torch.distributed as dist
+
+    return [dist.new_group([q, q + 1]) for q in range(world - 1)]
+
+
+def interface_slices(part: SlabPartition, indptr: torch.Tensor):
+    """Value-block ranges (relative to the window base) of the lower/upper interface planes."""
+    ip = indptr
+    base = int(ip[part.row_begin])
+    out = {}
+    for name, rr in (("lower", part.lower), ("upper", part.upper)):
+        if rr is not None:
+            out[name] = (int(ip[rr[0]]) - base, int(ip[rr[1]]) - base)
+    return out
+
+
+def bc_diagonal_fixups(part: SlabPartition, indptr: torch.Tensor, indices: torch.Tensor, marker: torch.Tensor | None,
+                       bs: int) -> torch.Tensor | None:
+    """Flat value indices (window-relative) of Dirichlet diagonal entries on interface rows."""
+    if marker is None:
+        return None
+    idx = []
+    base = int(indptr[part.row_begin])
+    for rr in (part.lower, part.upper):
+        if rr is None:
+            continue
+        rows = torch.arange(rr[0], rr[1], device=indptr.device)
+        m = marker.reshape(-1, bs)[rows]  # [nrows, bs]
+        hit_rows = rows[m.any(1)]
+        for r in hit_rows.tolist():
+            b, e = int(indptr[r]), int(indptr[r + 1])
+            cols = indices[b:e]
+            s = b + int(torch.nonzero(cols == r)[0, 0])
+            for i in range(bs):
+                if int(marker[r * bs + i]):
+                    idx.append((s - base) * bs * bs + i * bs + i)
+    if not idx:
+        return None
+    return torch.tensor(idx, dtype=torch.int64, device=indptr.device)
+
+
+def exchange_interfaces(part: SlabPartition, values: torch.Tensor, slices: dict, groups, fixups=None,
+                        diagonal: float = 1.0):
+    """Sum the interface-plane rows with the slab neighbours (2-rank all-reduces), then reset the
+    Dirichlet diagonals of interface rows. `values` = the window's [nblocks_window, bs, bs]."""
+    import torch.distributed as dist
+
+    flat = values.reshape(values.shape[0], -1)
+    steps = []
+    if part.lower is not None:
+        steps.append((part.rank - 1, slices["lower"]))  # boundary q = rank-1
+    if part.upper is not None:
+        steps.append((part.rank, slices["upper"]))  # boundary q = rank
+    # phase order: even boundaries first, then odd — consistent on both sides of every boundary
+    for q, (b0, b1) in sorted(steps, key=lambda s: (s[0] % 2, s[0])):
+        slab = flat[b0:b1]
+        dist.all_reduce(slab, op=dist.ReduceOp.SUM, group=groups[q])
+    if fixups is not None:
+        values.view(-1)[fixups] = diagonal
+
+
+class SlabProblem:
+    """One rank's share of the config-E assembly on its GPU (bench.py at N > 1):
+    3-D P2 linear elasticity on the unit cube, E = E_range[global cell % 200], x = 0 clamped,
+    x = 1 prescribed. ``assemble()`` = local gather assembly + interface exchange."""
+
+    def __init__(self, n: int, rank: int, world: int, device, degree: int = 2, nu: float = 0.3, groups=None,
+                 cell_type=None):
+        from . import fem, mesh
+        from .la import MatrixCSR
+        from .materials import e_range
+
+        ct = mesh.CellType.tetrahedron if cell_type is None else cell_type
+        part = SlabPartition((n, n, n), degree, rank, world)
+        self.part = part
+        L = (1.0, 1.0, 1.0)
+        m_pat = mesh.create_box(L, (n, n, n), ct, device=device, z_range=(part.kp0, part.kp1))
+        m_asm = mesh.create_box(L, (n, n, n), ct, device=device, z_range=(part.k0, part.k1))
+        nloc = part.num_local_nodes
+        dof_pat = part.to_local(fem._structured_dofmap(m_pat, degree)[0])
+        dof_asm = part.to_local(fem._structured_dofmap(m_asm, degree)[0])
+        V_pat = fem.FunctionSpace.from_dofmap(m_pat, degree, 3, dof_pat, nloc)
+        V = fem.FunctionSpace.from_dofmap(m_asm, degree, 3, dof_asm, nloc)
+        xs = fem._structured_node_coordinates(m_asm, degree)
+        V._x = xs[part.node_offset:part.node_offset + nloc].contiguous()
+        del xs
+        a_pat = fem.LinearElasticity(V_pat, E=1.0, nu=nu)
+        pat = fem.create_matrix(a_pat)
+        self.A = MatrixCSR(pat.indptr, pat.indices, 3, window=(part.row_begin, part.row_end))
+        V_pat._adjacency = None  # the pattern's adjacency is not needed after create_matrix
+        cells_per_layer = n * n * (6 if ct == mesh.CellType.tetrahedron else 1)
+        cid = torch.arange(m_asm.num_cells, device=device, dtype=torch.int64) + part.k0 * cells_per_layer
+        E = torch.tensor(e_range(), dtype=torch.float64, device=device)[cid % 200]
+        self.a = fem.LinearElasticity(V, E=E, nu=nu)
+        left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
+        right = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.ones_like(x[0])))
+        self.bcs = [fem.dirichletbc(0.0, left, V), fem.dirichletbc([0.01, 0.0, 0.0], right, V)]
+        marker, _ = fem._combine_bcs(V, self.bcs)
+        self.V = V
+        fem.gather_plan(V, self.A, 0)
+        self.slices = interface_slices(part, self.A.indptr)
+        self.fixups = bc_diagonal_fixups(part, self.A.indptr, self.A.indices, marker, 3)
+        self.groups = groups if groups is not None else make_pair_groups(world)
+        self.num_cells = m_asm.num_cells
+        self.kernel_name = "k_cell_records + k_gather<3,10,4,4,2,0> + 2-rank all_reduce(SUM) per slab boundary"
+
+    def assemble(self):
+        from . import fem
+
+        fem.assemble_matrix(self.a, bcs=self.bcs, A=self.A)
+        exchange_interfaces(self.part, self.A.parts[0][2], self.slices, self.groups, self.fixups)

@@ -1,0 +1,64 @@
+"""The GPU slab path end to end on one card: 2 ranks share cuda:0, each runs the HIP gather
+kernel on its slab (femasm.parallel.SlabProblem) and the interface rows are summed with gloo
+(RCCL needs one GPU per rank; the 8-GPU RCCL run is the driver's). Every owned row must equal a
+single-process full-mesh GPU assembly."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "fem-libraries_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from femasm import fem, parallel
+
+    dev = torch.device("cuda", 0)
+    prob = parallel.SlabProblem(n, rank, world, dev)
+    prob.assemble()
+    torch.cuda.synchronize()
+    m, V, a, bcs = bench.build_problem(n, dev)
+    A = fem.assemble_matrix(a, bcs=bcs)
+    part = prob.part
+    ip_l = prob.A.indptr.cpu().numpy()
+    ix_l = prob.A.indices.cpu().numpy()
+    vl = prob.A.parts[0][2].cpu().numpy()
+    ip_g = A.indptr.cpu().numpy()
+    ix_g = A.indices.cpu().numpy()
+    vg = A.data.cpu().numpy()
+    w0 = ip_l[part.row_begin]
+    scale = np.abs(vg).max()
+    err = 0.0
+    for r in range(part.row_begin, part.row_end):
+        g = r + part.node_offset
+        assert np.array_equal(ix_l[ip_l[r]:ip_l[r + 1]] + part.node_offset, ix_g[ip_g[g]:ip_g[g + 1]])
+        err = max(err, float(np.abs(vl[ip_l[r] - w0:ip_l[r + 1] - w0] - vg[ip_g[g]:ip_g[g + 1]]).max()))
+    assert err <= 1e-12 * scale, f"rank {rank}: rel err {err / scale:.2e}"
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 6), (3, 7)])
+def test_slab_problem_gpu_gloo(world, n):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    mp.spawn(_worker, args=(world, _port(), n), nprocs=world, join=True)
