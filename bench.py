@@ -32,7 +32,7 @@ import torch  # noqa: E402
 
 # algorithmic bytes per P2-tet cell under the element-stream model:
 # 4*nn (dofmap) + 4*nv (geometry dofmap) + 8*gdim*nv (coords) + 8*n_w (E) + 16*ndof^2
-B_E_P2_TET = 4 * 10 + 4 * 4 + 8 * 3 * 4 + 8 * 1 + 16 * 30 * 30  # = 14,560
+B_E_P2_TET = 4 * 10 + 4 * 4 + 8 * 3 * 4 + 8 * 1 + 16 * 30 * 30  # = 14,560 (bytes_per_cell(CONFIGS["E"]))
 HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, Chip-level parameters)
 
 
@@ -41,21 +41,64 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def build_problem(n, dev, z_range=None):
+# BASELINE.json configs. The bench line is config E's mesh with linear
+# elasticity ("E"); the others are available with --config for DESIGN.md measurements.
+CONFIGS = {
+    "A": dict(cell="triangle", degree=1, n=71, qdeg=1, label="2-D P1 tri, 71x71x2 (reference mechanic2d J, d=0)"),
+    "B": dict(cell="quadrilateral", degree=2, n=1000, qdeg=None, label="2-D Q2 quad, 1000x1000"),
+    "C": dict(cell="tetrahedron", degree=1, n=119, qdeg=None, label="3-D P1 tet, 119^3x6"),
+    "D": dict(cell="hexahedron", degree=3, n=58, qdeg=None, label="3-D Q3 hex, 58^3 (192x192 local)"),
+    "Dq2": dict(cell="hexahedron", degree=2, n=58, qdeg=None, label="3-D Q2 hex, 58^3 (81x81 local)"),
+    "E": dict(cell="tetrahedron", degree=2, n=203, qdeg=None, label="3-D P2 tet, 203^3x6 (config E mesh)"),
+}
+
+
+def bytes_per_cell(cfg):
+    """SURVEY.md §8(d) element-stream model: 4 nn + 4 nv + 8 gdim nv + 8 n_w + 16 ndof^2."""
+    from femasm import fem, mesh
+
+    ct = mesh.CellType[cfg["cell"]]
+    gd, nv = mesh.GDIM[ct], mesh.NVERTS[ct]
+    nn = fem.num_nodes_of(ct, cfg["degree"])
+    nd = nn * gd
+    geom = 0 if cfg["degree"] == 1 else 4 * nv  # the geometry dofmap is the dofmap itself at degree 1
+    return 4 * nn + geom + 8 * gd * nv + 8 + 16 * nd * nd
+
+
+def build_problem(n, dev, z_range=None, cfg=None):
     from femasm import fem, mesh
 
     from femasm.materials import e_range
 
-    m = mesh.create_box((1.0, 1.0, 1.0), (n, n, n), mesh.CellType.tetrahedron, device=dev, z_range=z_range)
-    V = fem.functionspace(m, ("Lagrange", 2, (3,)))
-    ncell_global0 = (z_range[0] if z_range else 0) * n * n * 6
+    cfg = cfg or CONFIGS["E"]
+    ct = mesh.CellType[cfg["cell"]]
+    if mesh.GDIM[ct] == 2:
+        m = mesh.create_rectangle((1.0, 1.0), (n, n), ct, device=dev)
+    else:
+        m = mesh.create_box((1.0, 1.0, 1.0), (n, n, n), ct, device=dev, z_range=z_range)
+    gd = m.gdim
+    V = fem.functionspace(m, ("Lagrange", cfg["degree"], (gd,)))
+    per_layer = n * n * (6 if ct == mesh.CellType.tetrahedron else 1)
+    ncell_global0 = (z_range[0] if z_range else 0) * per_layer
     cid = torch.arange(m.num_cells, device=dev, dtype=torch.int64) + ncell_global0
     E = torch.tensor(e_range(), dtype=torch.float64, device=dev)[cid % 200]
-    a = fem.form(fem.LinearElasticity(V, E=E, nu=0.3))
+    a = fem.form(fem.LinearElasticity(V, E=E, nu=0.3, quadrature_degree=cfg["qdeg"]))
     left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
     right = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.ones_like(x[0])))
-    bcs = [fem.dirichletbc(0.0, left, V), fem.dirichletbc([0.01, 0.0, 0.0], right, V)]
+    bcs = [fem.dirichletbc(0.0, left, V), fem.dirichletbc([0.01] + [0.0] * (gd - 1), right, V)]
     return m, V, a, bcs
+
+
+def measured_traffic(config: str, n: int, world: int):
+    """HBM bytes per assembly launch from the committed rocprofv3 PMC summary of the same workload
+    (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE, k_cell_records + k_gather), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if world != 1 or not os.path.exists(path):
+        return None
+    rec = json.load(open(path)).get(f"{config}:{n}")
+    if not rec:
+        return None
+    return {"bytes": rec["bytes"], "GB": round(rec["bytes"] / 1e9, 2), "source": rec["source"]}
 
 
 def cpu_baseline(sample_n: int, reps: int):
@@ -92,7 +135,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=203, help="cubes per side (config E: 203)")
+    ap.add_argument("--config", default="E", choices=sorted(CONFIGS))
+    ap.add_argument("--n", type=int, default=None, help="cells per side (default: the config's)")
     ap.add_argument("--method", default="gather", choices=["gather", "scatter"])
     ap.add_argument("--cpu-sample-n", type=int, default=24)
     ap.add_argument("--cpu-reps", type=int, default=7)
@@ -112,7 +156,9 @@ def main():
 
     from femasm import fem
 
-    n = args.n
+    cfg = CONFIGS[args.config]
+    n = args.n or cfg["n"]
+    b_e = bytes_per_cell(cfg)
     t0 = time.time()
     if world > 1:
         from femasm import parallel
@@ -122,7 +168,7 @@ def main():
         ncells_local = prob.num_cells
         kernel_name = prob.kernel_name
     else:
-        m, V, a, bcs = build_problem(n, dev)
+        m, V, a, bcs = build_problem(n, dev, cfg=cfg)
         A = fem.create_matrix(a)
         for part in range(len(A.parts)):
             fem.gather_plan(V, A, part)
@@ -166,7 +212,12 @@ def main():
 
     ms_per_step = elapsed / args.steps * 1e3
     melem_s = ncells_total / (ms_per_step * 1e-3) / 1e6
-    achieved = B_E_P2_TET * ncells_local / (launch_ms * 1e-3) / 1e9  # per-GPU kernel GB/s (algorithmic)
+    achieved = b_e * ncells_local / (launch_ms * 1e-3) / 1e9  # per-GPU GB/s, SURVEY §8(d) model
+    # secondary figure: compulsory 16 * nnz / ncells (zero-fill + accumulate of each value)
+    nnz_local = (A.nnz if world == 1 else prob.A.parts[0][2].numel())
+    compulsory = 16.0 * nnz_local / ncells_local
+    achieved_c = compulsory * ncells_local / (launch_ms * 1e-3) / 1e9
+    traffic = measured_traffic(args.config, n, world)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -177,6 +228,12 @@ def main():
                          f"median of {args.cpu_reps} runs ({t:.2f} s each), 1 thread"}
 
     if rank == 0:
+        workload = (f"config {args.config}: {cfg['label']} — linear-elasticity J, {ncells_total} cells, "
+                    f"E=E_range[cell%200], nu=0.3, x=0 clamped / x=1 prescribed, BSR(gdim) global matrix")
+        if args.config == "E":
+            workload = (f"config E mesh, linear elasticity J: unit cube {n}^3 x 6 Kuhn tets, P2 "
+                        f"({ncells_total} cells, {(2 * n + 1) ** 3 * 3} dofs), E=E_range[cell%200], "
+                        f"nu=0.3, x=0 clamped / x=1 prescribed, BSR(3) global matrix")
         out = {
             "metric": "Melements/s assembled + achieved HBM GB/s, 3D P2 elasticity at 1/2/4/8 GPUs",
             "value": round(melem_s, 3),
@@ -191,15 +248,18 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "hbm_GBps_algorithmic": round(achieved * world, 1),
-            "config": {"workload": f"config E mesh, linear elasticity J: unit cube {n}^3 x 6 Kuhn tets, P2 "
-                                   f"({ncells_total} cells, {(2 * n + 1) ** 3 * 3} dofs), E=E_range[cell%200], "
-                                   f"nu=0.3, x=0 clamped / x=1 prescribed, BSR(3) global matrix",
-                       "method": args.method, "quadrature_points": 4,
-                       "parallelism": f"z-slabs x{world}" if world > 1 else "single GPU"},
+            "config": {"workload": workload, "method": args.method,
+                       "parallelism": f"z-slabs x{world} (RCCL 2-rank all-reduce per boundary)" if world > 1
+                       else "single GPU"},
+            # achieved = SURVEY §8(d) element-stream bytes per cell (B_e) x cells / live event time of one
+            # assembly launch (k_cell_records + k_gather) on this rank; the gather algorithm moves far fewer
+            # bytes than that model, so frac can exceed 1 — see "compulsory" and "traffic" (DESIGN.md §3).
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                         "kernel": "k_gather<3,10,4,4,2,0> (P2 tet row-gather)" if world == 1 else None,
-                         "bytes_per_cell": B_E_P2_TET, "launch_ms": round(launch_ms, 4)},
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         "kernel": "k_cell_records + k_gather (row-gather assembly launch)",
+                         "bytes_per_cell": b_e, "launch_ms": round(launch_ms, 4),
+                         "compulsory": {"bytes_per_cell": round(compulsory, 1), "achieved": round(achieved_c, 1),
+                                        "frac": round(achieved_c / HBM_PEAK_GBPS, 4)}},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

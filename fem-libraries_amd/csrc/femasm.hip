@@ -1254,15 +1254,280 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
 }
 
 // ------------------------------------------------------------------------------------ vectors (next rows)
-extern "C" int fa_assemble_vector(const fa_mesh* mesh, const fa_form* form, double* b, void* stream) {
-  (void)mesh; (void)form; (void)b; (void)stream;
-  return fail(FA_E_UNSUPPORTED, "fa_assemble_vector: not implemented yet");
+// Damage-law stress at the single quadrature point, multiplied by w: restated from asym_stress
+// (hand version, MFEM/mechanic2d/asym_elasto_damage_model.cc:207-329). strain = (e00, e11, e01).
+__device__ __forceinline__ void damage_stress(double s00, double s11, double s01, double l, double m, double d,
+                                              double w, double (&sig)[2][2]) {
+  const double limit = 1.e-12, mlimit = -1.e-12;
+  sig[0][0] = sig[0][1] = sig[1][0] = sig[1][1] = 0.0;
+  if (d > 0.0) {
+    double I1 = s00 + s11, I2 = s01 * s01 - s00 * s11;
+    if (I1 > limit || I2 > limit || I1 < mlimit || I2 < mlimit) {
+      double delta = I1 * I1 + 4.0 * I2;
+      double r = sqrt(fmax(0.0, delta));
+      double ev0 = 0.5 * (I1 + r), ev1 = 0.5 * (I1 - r);
+      double a1 = ev0 >= 0.0 ? 1.0 : 0.0, a2 = ev1 >= 0.0 ? 1.0 : 0.0, a = (ev0 + ev1) >= 0.0 ? 1.0 : 0.0;
+      if (!((d == 1.0) && (a == 1.0) && (a1 == 1.0) && (a2 == 1.0))) {
+        double V00, V01, V10, V11;
+        if (fabs(s01) > limit) {
+          V00 = ev0 - s11; V01 = ev1 - s11; V10 = V11 = s01;
+          double n0 = sqrt(V00 * V00 + V10 * V10), n1 = sqrt(V01 * V01 + V11 * V11);
+          V00 /= n0; V10 /= n0; V01 /= n1; V11 /= n1;
+        } else {
+          V00 = V11 = 1.0; V10 = V01 = 0.0;
+        }
+        double temp = 2.0 * m * w, gam = 0.5 * l / m;
+        double c = 1.0 - a * d, c1 = 1.0 - a1 * d, c2 = 1.0 - a2 * d;
+        double D0 = temp * (c1 + gam * c), D1 = temp * gam * c, D2 = temp * (c2 + gam * c);
+        double e0 = D0 * ev0 + D1 * ev1, e1 = D1 * ev0 + D2 * ev1;
+        sig[0][0] = V00 * e0 * V00 + V01 * e1 * V01;
+        sig[1][1] = V10 * e0 * V10 + V11 * e1 * V11;
+        sig[0][1] = sig[1][0] = V00 * e0 * V10 + V01 * e1 * V11;
+      }
+    }
+  } else {
+    double m2plw = w * (2.0 * m + l), lw = l * w;
+    sig[0][0] = m2plw * s00 + lw * s11;
+    sig[1][1] = m2plw * s11 + lw * s00;
+    sig[0][1] = sig[1][0] = w * m * (s01 + s01);
+  }
 }
 
-extern "C" int fa_apply_lifting(const fa_mesh* mesh, const fa_form* form, double* b, const int8_t* bc, const double* g,
-                                const double* x0, double alpha, void* stream) {
-  (void)mesh; (void)form; (void)b; (void)bc; (void)g; (void)x0; (void)alpha; (void)stream;
-  return fail(FA_E_UNSUPPORTED, "fa_apply_lifting: not implemented yet");
+// geometry at quadrature point q of cell c: Jinv and |det J| (affine simplex: constant)
+template <int GD, int NV>
+__device__ __forceinline__ double cell_geometry_q(const MeshView& M, int64_t c, const double* gdphi_q,
+                                                  double (&Ji)[GD][GD]) {
+  if constexpr (NV == GD + 1) {
+    return fabs(simplex_geometry<GD>(M, c, Ji));
+  } else {
+    double xv[NV][GD];
+    const int32_t* gv = M.geom + c * NV;
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int i = 0; i < GD; ++i) xv[v][i] = M.x[(int64_t)gv[v] * GD + i];
+    return fabs(tensor_geometry<GD, NV>(xv, gdphi_q, Ji));
+  }
+}
+
+// Residual b[a] += sum over the cells of node a of int sigma(u):eps(phi_a e_i) - f.phi_a e_i.
+// One thread per node (node-parallel gather through the adjacency): deterministic, one write per dof.
+// Ts: tables of the sigma term's rule (the form's degree; the reference's `dxx`), Tf: the load
+// term's rule (degree 2p; the reference's default `dx`).
+template <int GD, int NV, int MAT>
+__global__ __launch_bounds__(256) void k_vector(MeshView M, FormView F, DevTables Ts, DevTables Tf,
+                                                const int64_t* __restrict__ adj_ptr,
+                                                const int32_t* __restrict__ adj_idx, double* __restrict__ b) {
+  const int nn = M.nn;
+  for (int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; a < M.nnodes; a += (int64_t)gridDim.x * blockDim.x) {
+    double r[GD];
+#pragma unroll
+    for (int i = 0; i < GD; ++i) r[i] = 0.0;
+    for (int64_t j = adj_ptr[a]; j < adj_ptr[a + 1]; ++j) {
+      const int32_t p = adj_idx[j];
+      const int64_t c = p / nn;
+      const int aloc = p % nn;
+      const int32_t* cn = M.cells + c * nn;
+      if (F.u) {
+        if constexpr (MAT == FA_ASYM_DAMAGE) {
+          double g[3][2], w, H[3][3];
+          damage_cell(M, F, c, g, w, H);  // gradients + weight (H unused here)
+          double lam, mu;
+          cell_lame(F, c, lam, mu);
+          double gr[2][2] = {{0.0, 0.0}, {0.0, 0.0}}, dq = 0.0;
+          for (int bb = 0; bb < 3; ++bb) {
+            int64_t n = cn[bb];
+            double u0 = F.u[n * 2], u1 = F.u[n * 2 + 1];
+            gr[0][0] += u0 * g[bb][0]; gr[0][1] += u0 * g[bb][1];
+            gr[1][0] += u1 * g[bb][0]; gr[1][1] += u1 * g[bb][1];
+            if (F.d) dq += F.d[n];
+          }
+          double sig[2][2];
+          damage_stress(gr[0][0], gr[1][1], 0.5 * (gr[0][1] + gr[1][0]), lam, mu, dq * (1.0 / 3.0), w, sig);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) r[i] += sig[i][0] * g[aloc][0] + sig[i][1] * g[aloc][1];
+        } else {
+          double lam, mu;
+          cell_lame(F, c, lam, mu);
+          for (int q = 0; q < Ts.nq; ++q) {
+            double Ji[GD][GD];
+            const double wd = Ts.wq[q] * cell_geometry_q<GD, NV>(M, c, Ts.gdphi + (size_t)q * NV * GD, Ji);
+            double gu[GD][GD];
+#pragma unroll
+            for (int i = 0; i < GD; ++i)
+#pragma unroll
+              for (int k = 0; k < GD; ++k) gu[i][k] = 0.0;
+            double ga[GD];
+            for (int bb = 0; bb < nn; ++bb) {
+              double gb[GD];
+              phys_grad<GD>(Ts.dphi + ((size_t)q * nn + bb) * GD, Ji, gb);
+              if (bb == aloc)
+#pragma unroll
+                for (int k = 0; k < GD; ++k) ga[k] = gb[k];
+              const int64_t n = cn[bb];
+#pragma unroll
+              for (int i = 0; i < GD; ++i) {
+                const double ui = F.u[n * GD + i];
+#pragma unroll
+                for (int k = 0; k < GD; ++k) gu[i][k] += ui * gb[k];
+              }
+            }
+            double tr = 0.0;
+#pragma unroll
+            for (int i = 0; i < GD; ++i) tr += gu[i][i];
+#pragma unroll
+            for (int i = 0; i < GD; ++i) {
+              double s = 0.0;
+#pragma unroll
+              for (int k = 0; k < GD; ++k) {
+                const double sig = mu * (gu[i][k] + gu[k][i]) + (i == k ? lam * tr : 0.0);
+                s += sig * ga[k];
+              }
+              r[i] += wd * s;
+            }
+          }
+        }
+      }
+      if (F.f) {
+        for (int q = 0; q < Tf.nq; ++q) {
+          double Ji[GD][GD];
+          const double wd = Tf.wq[q] * cell_geometry_q<GD, NV>(M, c, Tf.gdphi + (size_t)q * NV * GD, Ji);
+          double fq[GD];
+#pragma unroll
+          for (int i = 0; i < GD; ++i) fq[i] = 0.0;
+          for (int bb = 0; bb < nn; ++bb) {
+            const double ph = Tf.phi[(size_t)q * nn + bb];
+            const int64_t n = cn[bb];
+#pragma unroll
+            for (int i = 0; i < GD; ++i) fq[i] += F.f[n * GD + i] * ph;
+          }
+          const double pa = Tf.phi[(size_t)q * nn + aloc] * wd;
+#pragma unroll
+          for (int i = 0; i < GD; ++i) r[i] -= fq[i] * pa;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < GD; ++i) b[a * GD + i] += r[i];
+  }
+}
+
+// dolfinx apply_lifting with one J form: b[a] -= alpha * sum over the cells of a that hold bc dofs
+// of K_e[a, j] (g_j - x0_j) for constrained dofs j (element matrices, as dolfinx does per cell).
+template <int GD, int NV, int MAT>
+__global__ __launch_bounds__(256) void k_lifting(MeshView M, FormView F, DevTables T, const int64_t* __restrict__ adj_ptr,
+                                                 const int32_t* __restrict__ adj_idx, const int8_t* __restrict__ bc,
+                                                 const double* __restrict__ g, const double* __restrict__ x0,
+                                                 double alpha, double* __restrict__ b) {
+  const int nn = M.nn;
+  for (int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; a < M.nnodes; a += (int64_t)gridDim.x * blockDim.x) {
+    double r[GD];
+#pragma unroll
+    for (int i = 0; i < GD; ++i) r[i] = 0.0;
+    for (int64_t j = adj_ptr[a]; j < adj_ptr[a + 1]; ++j) {
+      const int32_t p = adj_idx[j];
+      const int64_t c = p / nn;
+      const int aloc = p % nn;
+      const int32_t* cn = M.cells + c * nn;
+      bool any = false;
+      for (int bb = 0; bb < nn && !any; ++bb)
+#pragma unroll
+        for (int k = 0; k < GD; ++k) any |= bc[(int64_t)cn[bb] * GD + k] != 0;
+      if (!any) continue;
+      for (int bb = 0; bb < nn; ++bb) {
+        const int64_t nb = cn[bb];
+        bool hit = false;
+#pragma unroll
+        for (int k = 0; k < GD; ++k) hit |= bc[nb * GD + k] != 0;
+        if (!hit) continue;
+        double K[GD][GD];
+        if constexpr (MAT == FA_ASYM_DAMAGE) {
+          if constexpr (GD == 2) {
+            double gg[3][2], w, H[3][3];
+            damage_cell(M, F, c, gg, w, H);
+            double ga[2] = {gg[aloc][0], gg[aloc][1]}, gb[2] = {gg[bb][0], gg[bb][1]};
+            damage_block(ga, gb, w, H, K);
+          }
+        } else {
+          double lam, mu;
+          cell_lame(F, c, lam, mu);
+          double G[GD][GD];
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int k = 0; k < GD; ++k) G[i][k] = 0.0;
+          for (int q = 0; q < T.nq; ++q) {
+            double Ji[GD][GD];
+            const double wd = T.wq[q] * cell_geometry_q<GD, NV>(M, c, T.gdphi + (size_t)q * NV * GD, Ji);
+            double ga[GD], gb[GD];
+            phys_grad<GD>(T.dphi + ((size_t)q * nn + aloc) * GD, Ji, ga);
+            phys_grad<GD>(T.dphi + ((size_t)q * nn + bb) * GD, Ji, gb);
+#pragma unroll
+            for (int i = 0; i < GD; ++i)
+#pragma unroll
+              for (int k = 0; k < GD; ++k) G[i][k] += wd * ga[i] * gb[k];
+          }
+          lin_block<GD>(G, lam, mu, K);
+        }
+#pragma unroll
+        for (int k = 0; k < GD; ++k) {
+          if (!bc[nb * GD + k]) continue;
+          const double v = g[nb * GD + k] - (x0 ? x0[nb * GD + k] : 0.0);
+#pragma unroll
+          for (int i = 0; i < GD; ++i) r[i] += K[i][k] * v;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < GD; ++i) b[a * GD + i] -= alpha * r[i];
+  }
+}
+
+#define FA_VEC_DISPATCH(KERNEL, ...)                                                              \
+  do {                                                                                            \
+    const int g_ = grid_for(mesh->nnodes);                                                        \
+    const bool dam_ = form->kind == FA_ASYM_DAMAGE;                                               \
+    switch (mesh->cell_type) {                                                                    \
+      case FA_TRIANGLE:                                                                           \
+        if (dam_) KERNEL<2, 3, FA_ASYM_DAMAGE><<<g_, 256, 0, s>>>(__VA_ARGS__);                   \
+        else KERNEL<2, 3, 0><<<g_, 256, 0, s>>>(__VA_ARGS__);                                     \
+        break;                                                                                    \
+      case FA_QUADRILATERAL: KERNEL<2, 4, 0><<<g_, 256, 0, s>>>(__VA_ARGS__); break;               \
+      case FA_TETRAHEDRON: KERNEL<3, 4, 0><<<g_, 256, 0, s>>>(__VA_ARGS__); break;                 \
+      case FA_HEXAHEDRON: KERNEL<3, 8, 0><<<g_, 256, 0, s>>>(__VA_ARGS__); break;                  \
+    }                                                                                             \
+    LAUNCH_CHECK();                                                                               \
+  } while (0)
+
+extern "C" int fa_assemble_vector(const fa_mesh* mesh, const fa_form* form, const fa_adjacency* adj, double* b,
+                                  void* stream) {
+  int rc = check_mesh(mesh);
+  if (rc) return rc;
+  if (!adj || !adj->ptr || !adj->idx || !b) return fail(FA_E_ARG, "null argument");
+  FormView F;
+  if ((rc = form_view(mesh, form, F))) return rc;
+  DevTables Ts, Tf;
+  if ((rc = get_tables(mesh->cell_type, mesh->degree, form->qdeg, &Ts))) return rc;
+  if ((rc = get_tables(mesh->cell_type, mesh->degree, 2 * mesh->degree, &Tf))) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  MeshView M{mesh->cells, mesh->geom, mesh->x, mesh->ncells, mesh->nnodes, mesh->nn, mesh->nv, mesh->gdim};
+  if (mesh->nnodes > 0) FA_VEC_DISPATCH(k_vector, M, F, Ts, Tf, adj->ptr, adj->idx, b);
+  return FA_OK;
+}
+
+extern "C" int fa_apply_lifting(const fa_mesh* mesh, const fa_form* form, const fa_adjacency* adj, double* b,
+                                const int8_t* bc, const double* g, const double* x0, double alpha, void* stream) {
+  int rc = check_mesh(mesh);
+  if (rc) return rc;
+  if (!adj || !adj->ptr || !adj->idx || !b || !bc || !g) return fail(FA_E_ARG, "null argument");
+  FormView F;
+  if ((rc = form_view(mesh, form, F))) return rc;
+  DevTables T;
+  if ((rc = get_tables(mesh->cell_type, mesh->degree, form->qdeg, &T))) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  MeshView M{mesh->cells, mesh->geom, mesh->x, mesh->ncells, mesh->nnodes, mesh->nn, mesh->nv, mesh->gdim};
+  if (mesh->nnodes > 0) FA_VEC_DISPATCH(k_lifting, M, F, T, adj->ptr, adj->idx, bc, g, x0, alpha, b);
+  return FA_OK;
 }
 
 __global__ void k_set_bc(double* __restrict__ b, int64_t n, const int8_t* __restrict__ bc, const double* __restrict__ g,

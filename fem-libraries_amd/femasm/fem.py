@@ -367,7 +367,8 @@ class LinearElasticity:
     E: DG0 Function / per-cell tensor / float; nu: Constant / float. Alternatively lam & mu per cell."""
     kind = _lib.FA_LINEAR_ELASTICITY
 
-    def __init__(self, V: FunctionSpace, E=None, nu=0.3, lam=None, mu=None, quadrature_degree: int | None = None):
+    def __init__(self, V: FunctionSpace, E=None, nu=0.3, lam=None, mu=None, quadrature_degree: int | None = None,
+                 u=None, f=None):
         self.V = V
         nc = V.mesh.num_cells
         dev = V.mesh.device
@@ -378,7 +379,10 @@ class LinearElasticity:
         else:
             self.lam, self.mu = _cellwise(lam, nc, dev), _cellwise(mu, nc, dev)
         self.qdeg = -1 if quadrature_degree is None else int(quadrature_degree)
-        self.u = self.d = self.f = None
+        self.d = None
+        # state (residual / nonlinear tangents) and body force, per dof; Functions or tensors
+        self.u = None if u is None else (u.x if isinstance(u, Function) else u)
+        self.f = None if f is None else (f.x if isinstance(f, Function) else f)
 
 
 class AsymDamage(LinearElasticity):
@@ -388,9 +392,8 @@ class AsymDamage(LinearElasticity):
     u: displacement Function, d: damage (P1 scalar Function or per-node tensor)."""
     kind = _lib.FA_ASYM_DAMAGE
 
-    def __init__(self, V: FunctionSpace, E=None, nu=0.3, u=None, d=None, lam=None, mu=None):
-        super().__init__(V, E=E, nu=nu, lam=lam, mu=mu, quadrature_degree=1)
-        self.u = None if u is None else (u.x if isinstance(u, Function) else u)
+    def __init__(self, V: FunctionSpace, E=None, nu=0.3, u=None, d=None, lam=None, mu=None, f=None):
+        super().__init__(V, E=E, nu=nu, lam=lam, mu=mu, quadrature_degree=1, u=u, f=f)
         self.d = None if d is None else (d.x if isinstance(d, Function) else d)
 
 
@@ -524,3 +527,55 @@ def tabulate_cells(a, c0: int = 0, ncells: int | None = None) -> torch.Tensor:
     _lib.check(L.fa_tabulate_cells(ctypes.byref(fm), ctypes.byref(ff), c0, nc, Ae.data_ptr(),
                                    _lib.stream_handle(V.mesh.device)), "fa_tabulate_cells")
     return Ae
+
+
+def assemble_vector(L, b: torch.Tensor | None = None) -> torch.Tensor:
+    """Residual of the form's constitutive law: b += int sigma(u):eps(v) dxx - int f.v dx
+    (dolfinx.fem.assemble_vector of the reference F, FEniCSx/mechanic2d/asym_elasto_damage_model.cc:825;
+    MFEM damIntegrator::AssembleElementVector :559-637). u, f are the form's `u` / `f` (None = 0)."""
+    V = L.V
+    if b is None:
+        b = torch.zeros(V.num_dofs, dtype=torch.float64, device=V.mesh.device)
+    Lb = _lib.load()
+    fm = V._fa_mesh()
+    ff = _fa_form(L)
+    adj = V._fa_adjacency()
+    _lib.check(Lb.fa_assemble_vector(ctypes.byref(fm), ctypes.byref(ff), ctypes.byref(adj), b.data_ptr(),
+                                     _lib.stream_handle(V.mesh.device)), "fa_assemble_vector")
+    return b
+
+
+def apply_lifting(b: torch.Tensor, a: list, bcs: list, x0: list | None = None, alpha: float = 1.0, scale=None):
+    """dolfinx apply_lifting: b -= alpha * A (g - x0) over constrained columns, with the cell
+    matrices of a[0] (the reference calls it with alpha = -1, :827)."""
+    if scale is not None:
+        alpha = scale
+    form_ = a[0]
+    V = form_.V
+    marker, g = _combine_bcs(V, bcs[0])
+    if marker is None:
+        return b
+    x = None if not x0 else (x0[0].x if isinstance(x0[0], Function) else x0[0])
+    Lb = _lib.load()
+    fm = V._fa_mesh()
+    ff = _fa_form(form_)
+    adj = V._fa_adjacency()
+    _lib.check(Lb.fa_apply_lifting(ctypes.byref(fm), ctypes.byref(ff), ctypes.byref(adj), b.data_ptr(),
+                                   marker.data_ptr(), g.data_ptr(), _lib.ptr(x), float(alpha),
+                                   _lib.stream_handle(V.mesh.device)), "fa_apply_lifting")
+    return b
+
+
+def set_bc(b: torch.Tensor, bcs: list, x0=None, alpha: float = 1.0, scale=None):
+    """dolfinx set_bc: b[bc dofs] = alpha * (g - x0) (the reference: alpha = -1, x0 = u, :836)."""
+    if scale is not None:
+        alpha = scale
+    if not bcs:
+        return b
+    V = bcs[0].V
+    marker, g = _combine_bcs(V, bcs)
+    x = None if x0 is None else (x0.x if isinstance(x0, Function) else x0)
+    Lb = _lib.load()
+    _lib.check(Lb.fa_set_bc(b.data_ptr(), b.numel(), marker.data_ptr(), g.data_ptr(), _lib.ptr(x), float(alpha),
+                            _lib.stream_handle(V.mesh.device)), "fa_set_bc")
+    return b

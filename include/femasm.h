@@ -146,15 +146,18 @@ int fa_tabulate_cells(const fa_mesh* mesh, const fa_form* form, int64_t c0, int6
 int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, const fa_adjacency* adj, const fa_plan* plan,
                        const int8_t* bc, double diag, fa_bsr* A, int32_t flags, void* stream);
 
-/* Residual b += int sigma(u):eps(v) - f.v over all cells (b is ADDED into; zero it first). */
-int fa_assemble_vector(const fa_mesh* mesh, const fa_form* form, double* b, void* stream);
+/* Residual b += int sigma(u):eps(v) dx_q - int f.v dx_{2p} (b is ADDED into, like dolfinx
+ * assemble_vector; the reference zeroes it first). sigma term on the form's quadrature degree
+ * (the reference's `dxx`), load term on degree 2p (the reference's default `dx`). Node-parallel
+ * through the adjacency: deterministic, one write per dof. u / f may be NULL (= 0). */
+int fa_assemble_vector(const fa_mesh* mesh, const fa_form* form, const fa_adjacency* adj, double* b, void* stream);
 
 /* dolfinx apply_lifting with one form: b[i] -= alpha * sum_j A_ij (g_j - x0_j) over bc
  * columns j, computed cell by cell with the cell matrices (bc rows i get no contribution;
  * set_bc overwrites them). The reference calls it with alpha = -1
  * (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:827). g, x0 per dof (x0 may be NULL = 0). */
-int fa_apply_lifting(const fa_mesh* mesh, const fa_form* form, double* b, const int8_t* bc, const double* g,
-                     const double* x0, double alpha, void* stream);
+int fa_apply_lifting(const fa_mesh* mesh, const fa_form* form, const fa_adjacency* adj, double* b, const int8_t* bc,
+                     const double* g, const double* x0, double alpha, void* stream);
 
 /* b[i] = alpha * (g[i] - x0[i]) on bc dofs (x0 may be NULL). ndofs = nnodes*bs. */
 int fa_set_bc(double* b, int64_t ndofs, const int8_t* bc, const double* g, const double* x0, double alpha,

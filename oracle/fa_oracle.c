@@ -762,3 +762,124 @@ int ora_cell_matrices_elasticity(const ora_mesh* M, const double* lam, const dou
   free(dphi); free(gdphi);
   return 0;
 }
+
+/* ---------------------------------------------------------------- residual & lifting */
+/* dolfinx assemble_vector of F = inner(sigma(u), eps(v)) dx_qs - inner(f, v) dx_qf restated
+ * per cell with Voigt vectors: b_e = sum_q w|J| B^T sigma_v - sum_q w|J| N^T f(q); b[dofs] += b_e.
+ * kind 0: linear sigma = D B u;  kind 1: reference damage law (P1 tri, centroid, asym_stress).
+ * u, f per dof (may be NULL); dnode per node (kind 1). qs < 0: estimated degree. */
+int ora_assemble_residual(const ora_mesh* M, int kind, const double* lam, const double* mu, const double* u,
+                          const double* dnode, const double* f, int qs, double* b) {
+  int gd = M->gdim, nn = M->nn, nv = M->nv, nd = nn * gd, nvo = gd == 2 ? 3 : 6;
+  if (qs < 0) qs = simplex(M->cell_type) ? 2 * (M->degree - 1) : 2 * M->degree;
+  if (kind == 1) qs = 1;
+  int qf = 2 * M->degree;
+  static double ps[ORA_MAXQ * 3], ws[ORA_MAXQ], pf[ORA_MAXQ * 3], wf[ORA_MAXQ];
+  int nqs = ora_quadrature(M->cell_type, qs, ps, ws);
+  int nqf = ora_quadrature(M->cell_type, qf, pf, wf);
+  double* dphi_s = (double*)malloc(sizeof(double) * nqs * nn * gd);
+  double* gdphi_s = (double*)malloc(sizeof(double) * nqs * nv * gd);
+  double* phi_f = (double*)malloc(sizeof(double) * nqf * nn);
+  double* gdphi_f = (double*)malloc(sizeof(double) * nqf * nv * gd);
+  ora_tabulate(M->cell_type, M->degree, nqs, ps, NULL, dphi_s);
+  ora_tabulate(M->cell_type, 1, nqs, ps, NULL, gdphi_s);
+  ora_tabulate(M->cell_type, M->degree, nqf, pf, phi_f, NULL);
+  ora_tabulate(M->cell_type, 1, nqf, pf, NULL, gdphi_f);
+  double* be = (double*)malloc(sizeof(double) * nd);
+  double* B = (double*)malloc(sizeof(double) * nvo * nd);
+  double Jinv[9], g[ORA_MAXN * 3], D[36], xv[8 * 3];
+  for (int64_t c = 0; c < M->ncells; ++c) {
+    const int32_t* nodes = &M->cells[c * nn];
+    memset(be, 0, sizeof(double) * nd);
+    for (int v = 0; v < nv; ++v)
+      for (int d = 0; d < gd; ++d) xv[v * gd + d] = M->x[(int64_t)M->geom[c * nv + v] * gd + d];
+    if (u) {
+      for (int q = 0; q < nqs; ++q) {
+        double det = jacobian(gd, nv, &gdphi_s[q * nv * gd], xv, Jinv);
+        double w = ws[q] * fabs(det);
+        phys_grads(gd, nn, &dphi_s[q * nn * gd], Jinv, g);
+        voigt_B(gd, nn, g, B);
+        double ev[6] = {0}, sv[6] = {0};
+        for (int k = 0; k < nvo; ++k)
+          for (int j = 0; j < nd; ++j) ev[k] += B[k * nd + j] * u[(int64_t)nodes[j / gd] * gd + j % gd];
+        if (kind == 1) {
+          double dq = 0;
+          for (int a = 0; a < 3; ++a) dq += dnode[nodes[a]] / 3.0;
+          double strain[3] = {ev[0], ev[1], 0.5 * ev[2]}, sig[3];
+          ora_damage_stress(strain, lam[c], mu[c], dq, w, sig);
+          sv[0] = sig[0]; sv[1] = sig[1]; sv[2] = sig[2];
+          for (int i = 0; i < nd; ++i)
+            for (int k = 0; k < nvo; ++k) be[i] += B[k * nd + i] * sv[k];
+        } else {
+          hooke_D(gd, lam[c], mu[c], D);
+          for (int k = 0; k < nvo; ++k)
+            for (int l = 0; l < nvo; ++l) sv[k] += D[k * nvo + l] * ev[l];
+          for (int i = 0; i < nd; ++i)
+            for (int k = 0; k < nvo; ++k) be[i] += w * B[k * nd + i] * sv[k];
+        }
+      }
+    }
+    if (f) {
+      for (int q = 0; q < nqf; ++q) {
+        double det = jacobian(gd, nv, &gdphi_f[q * nv * gd], xv, Jinv);
+        double w = wf[q] * fabs(det);
+        double fq[3] = {0, 0, 0};
+        for (int a = 0; a < nn; ++a)
+          for (int i = 0; i < gd; ++i) fq[i] += phi_f[q * nn + a] * f[(int64_t)nodes[a] * gd + i];
+        for (int a = 0; a < nn; ++a)
+          for (int i = 0; i < gd; ++i) be[a * gd + i] -= w * phi_f[q * nn + a] * fq[i];
+      }
+    }
+    for (int i = 0; i < nd; ++i) b[(int64_t)nodes[i / gd] * gd + i % gd] += be[i];
+  }
+  free(be); free(B); free(dphi_s); free(gdphi_s); free(phi_f); free(gdphi_f);
+  return 0;
+}
+
+/* dolfinx apply_lifting (one form, one bc set): for every cell holding a constrained dof,
+ * b[dofs] -= alpha * A_e (g - x0) restricted to constrained columns (FEniCSx/mechanic2d/
+ * asym_elasto_damage_model.cc:827 calls it with alpha = -1). kind as above (J form). */
+int ora_apply_lifting(const ora_mesh* M, int kind, const double* lam, const double* mu, const double* u,
+                      const double* dnode, int qdeg, const int8_t* bc, const double* gval, const double* x0,
+                      double alpha, double* b) {
+  int gd = M->gdim, nn = M->nn, nv = M->nv, nd = nn * gd;
+  if (qdeg < 0) qdeg = simplex(M->cell_type) ? 2 * (M->degree - 1) : 2 * M->degree;
+  static double pts[ORA_MAXQ * 3], wq[ORA_MAXQ];
+  int nq = ora_quadrature(M->cell_type, qdeg, pts, wq);
+  double* dphi = (double*)malloc(sizeof(double) * nq * nn * gd);
+  double* gdphi = (double*)malloc(sizeof(double) * nq * nv * gd);
+  ora_tabulate(M->cell_type, M->degree, nq, pts, NULL, dphi);
+  ora_tabulate(M->cell_type, 1, nq, pts, NULL, gdphi);
+  double* Ae = (double*)malloc(sizeof(double) * nd * nd);
+  double xv[8 * 3], vbc[ORA_MAXN * 3];
+  for (int64_t c = 0; c < M->ncells; ++c) {
+    const int32_t* nodes = &M->cells[c * nn];
+    int any = 0;
+    for (int i = 0; i < nd; ++i) {
+      int64_t dof = (int64_t)nodes[i / gd] * gd + i % gd;
+      vbc[i] = bc[dof] ? gval[dof] - (x0 ? x0[dof] : 0.0) : 0.0;
+      any |= bc[dof] != 0;
+    }
+    if (!any) continue;
+    memset(Ae, 0, sizeof(double) * nd * nd);
+    for (int v = 0; v < nv; ++v)
+      for (int d = 0; d < gd; ++d) xv[v * gd + d] = M->x[(int64_t)M->geom[c * nv + v] * gd + d];
+    if (kind == 1) {
+      double uc[6], dq = 0;
+      for (int a = 0; a < 3; ++a) {
+        for (int d = 0; d < 2; ++d) uc[a * 2 + d] = u ? u[(int64_t)nodes[a] * 2 + d] : 0.0;
+        dq += (dnode ? dnode[nodes[a]] : 0.0) / 3.0;
+      }
+      ora_damage_cell(xv, uc, dq, lam[c], mu[c], Ae);
+    } else {
+      ora_elasticity_cell(gd, nn, nq, wq, dphi, nv, gdphi, xv, lam[c], mu[c], Ae);
+    }
+    for (int i = 0; i < nd; ++i) {
+      double s = 0;
+      for (int j = 0; j < nd; ++j) s += Ae[i * nd + j] * vbc[j];
+      b[(int64_t)nodes[i / gd] * gd + i % gd] -= alpha * s;
+    }
+  }
+  free(Ae); free(dphi); free(gdphi);
+  return 0;
+}

@@ -62,6 +62,9 @@ def lib():
         L.ora_assemble_elasticity.argtypes = [ctypes.POINTER(_Mesh), P, P, ctypes.c_int, P, ctypes.c_double, P, P, P]
         L.ora_assemble_damage.argtypes = [ctypes.POINTER(_Mesh), P, P, P, P, P, ctypes.c_double, P, P, P]
         L.ora_cell_matrices_elasticity.argtypes = [ctypes.POINTER(_Mesh), P, P, ctypes.c_int, P]
+        L.ora_assemble_residual.argtypes = [ctypes.POINTER(_Mesh), ctypes.c_int, P, P, P, P, P, ctypes.c_int, P]
+        L.ora_apply_lifting.argtypes = [ctypes.POINTER(_Mesh), ctypes.c_int, P, P, P, P, ctypes.c_int, P, P, P,
+                                        ctypes.c_double, P]
         _lib = L
     return _lib
 
@@ -217,3 +220,45 @@ def bsr_to_dense(indptr, indices, values, nrows_nodes):
             c = indices[s]
             A[r * bs:(r + 1) * bs, c * bs:(c + 1) * bs] += values[s]
     return A
+
+
+def _opt(a, dtype=np.float64):
+    return None if a is None else np.ascontiguousarray(a, dtype=dtype)
+
+
+def assemble_residual(cell_type, degree, cells, geom, x, lam, mu, u=None, f=None, d=None, kind=0, qdeg=-1):
+    """dolfinx assemble_vector of inner(sigma(u), eps(v)) dxx - inner(f, v) dx (kind 1: damage law)."""
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    geom = np.ascontiguousarray(geom, dtype=np.int32)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    nc = cells.shape[0]
+    lam = np.ascontiguousarray(np.broadcast_to(lam, (nc,)), dtype=np.float64)
+    mu = np.ascontiguousarray(np.broadcast_to(mu, (nc,)), dtype=np.float64)
+    u, f, d = _opt(u), _opt(f), _opt(d)
+    nnodes = int(cells.max()) + 1
+    b = np.zeros(nnodes * _GDIM[cell_type])
+    m = _mesh_struct(cell_type, degree, cells, geom, x)
+    r = lib().ora_assemble_residual(ctypes.byref(m), kind, _p(lam), _p(mu), None if u is None else _p(u),
+                                    None if d is None else _p(d), None if f is None else _p(f), qdeg, _p(b))
+    assert r == 0
+    return b
+
+
+def apply_lifting(cell_type, degree, cells, geom, x, lam, mu, b, bc, g, x0=None, alpha=-1.0, u=None, d=None, kind=0,
+                  qdeg=-1):
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    geom = np.ascontiguousarray(geom, dtype=np.int32)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    nc = cells.shape[0]
+    lam = np.ascontiguousarray(np.broadcast_to(lam, (nc,)), dtype=np.float64)
+    mu = np.ascontiguousarray(np.broadcast_to(mu, (nc,)), dtype=np.float64)
+    b = np.array(b, dtype=np.float64, copy=True)
+    bc = np.ascontiguousarray(bc, dtype=np.int8)
+    g = np.ascontiguousarray(g, dtype=np.float64)
+    x0, u, d = _opt(x0), _opt(u), _opt(d)
+    m = _mesh_struct(cell_type, degree, cells, geom, x)
+    r = lib().ora_apply_lifting(ctypes.byref(m), kind, _p(lam), _p(mu), None if u is None else _p(u),
+                                None if d is None else _p(d), qdeg, _p(bc), _p(g), None if x0 is None else _p(x0),
+                                alpha, _p(b))
+    assert r == 0
+    return b

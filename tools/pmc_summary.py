@@ -23,3 +23,29 @@ for k, d in acc.items():
         if c == "WRITE_SIZE":
             extra = f"  ({mean / 1e6:.3f} GB)"
         print(f"  {c:24s} {mean:16.1f}{extra}  [{len(per)} dispatches]")
+
+
+def traffic_record(root, kernels=("k_gather", "k_cell_records")):
+    """HBM bytes per assembly launch: sum over the launch's kernels of FETCH_SIZE x 2 + WRITE_SIZE (KB)."""
+    tot = 0.0
+    for k, d in acc.items():
+        if not any(s in k for s in kernels):
+            continue
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            if c not in d:
+                continue
+            per = defaultdict(float)
+            for did, v in d[c]:
+                per[did] += v
+            mean = sum(per.values()) / len(per)
+            tot += (2.0 if c == "FETCH_SIZE" else 1.0) * mean * 1e3
+    return tot
+
+
+if len(sys.argv) > 3:  # pmc_summary.py ROOT KEY OUT_JSON: record traffic for bench.py
+    import json
+
+    key, out = sys.argv[2], sys.argv[3]
+    data = json.load(open(out)) if os.path.exists(out) else {}
+    data[key] = {"bytes": traffic_record(root), "source": f"rocprofv3 --pmc passes in {root} (tools/prof_passes.sh)"}
+    json.dump(data, open(out, "w"), indent=1)
