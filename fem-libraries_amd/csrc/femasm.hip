@@ -241,6 +241,23 @@ __device__ __forceinline__ double tensor_geometry(const double (&xv)[NV][GD], co
   return jac_inv<GD>(J, Ji);
 }
 
+// geometry at quadrature point q of cell c: Jinv and |det J| (affine simplex: constant)
+template <int GD, int NV>
+__device__ __forceinline__ double cell_geometry_q(const MeshView& M, int64_t c, const double* gdphi_q,
+                                                  double (&Ji)[GD][GD]) {
+  if constexpr (NV == GD + 1) {
+    return fabs(simplex_geometry<GD>(M, c, Ji));
+  } else {
+    double xv[NV][GD];
+    const int32_t* gv = M.geom + c * NV;
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int i = 0; i < GD; ++i) xv[v][i] = M.x[(int64_t)gv[v] * GD + i];
+    return fabs(tensor_geometry<GD, NV>(xv, gdphi_q, Ji));
+  }
+}
+
 // physical gradient g[d] = sum_k dphi[k] Ji[k][d]
 template <int GD>
 __device__ __forceinline__ void phys_grad(const double* dphi, const double (&Ji)[GD][GD], double (&g)[GD]) {
@@ -385,6 +402,110 @@ __device__ __forceinline__ int64_t find_slot(const int64_t* indptr, const int32_
   return -1;
 }
 
+// ------------------------------------------------------------------------------------ AD: neo-Hookean tangent
+// Forward-mode dual numbers, nested for second derivatives: the Hessian of a potential psi(F) is
+// taken entry by entry over the upper triangle, seeding x_i in the inner and x_j in the outer
+// level (the forward-over-forward pattern of the reference's MFEM AD,
+// MFEM/mechanic2d/autodiff/admfem.hpp:672-700: n(n+1)/2 evaluations; here n = gdim^2).
+template <class T>
+struct Dual {
+  T v, d;
+};
+template <class T>
+__device__ __forceinline__ Dual<T> operator+(const Dual<T>& a, const Dual<T>& b) { return {a.v + b.v, a.d + b.d}; }
+template <class T>
+__device__ __forceinline__ Dual<T> operator-(const Dual<T>& a, const Dual<T>& b) { return {a.v - b.v, a.d - b.d}; }
+template <class T>
+__device__ __forceinline__ Dual<T> operator*(const Dual<T>& a, const Dual<T>& b) { return {a.v * b.v, a.d * b.v + a.v * b.d}; }
+template <class T>
+__device__ __forceinline__ Dual<T> operator*(double s, const Dual<T>& a) { return {s * a.v, s * a.d}; }
+template <class T>
+__device__ __forceinline__ Dual<T> operator+(const Dual<T>& a, double s) { return {a.v + s, a.d}; }
+__device__ __forceinline__ double ad_inv(double x) { return 1.0 / x; }
+template <class T>
+__device__ __forceinline__ Dual<T> ad_inv(const Dual<T>& a) {
+  T r = ad_inv(a.v);
+  return {r, (-1.0) * (a.d * r * r)};
+}
+__device__ __forceinline__ double ad_log(double x) { return log(x); }
+template <class T>
+__device__ __forceinline__ Dual<T> ad_log(const Dual<T>& a) { return {ad_log(a.v), a.d * ad_inv(a.v)}; }
+
+// Compressible neo-Hookean potential psi(F) = mu/2 (I_C - 3) - mu ln J + lam/2 (ln J)^2,
+// F = I + grad u (2-D: plane strain, F33 = 1, so I_C - 3 = F:F - 2).
+template <int GD, class T>
+__device__ __forceinline__ T neo_psi(const T (&F)[GD * GD], double lam, double mu) {
+  T J, ff = F[0] * F[0];
+#pragma unroll
+  for (int k = 1; k < GD * GD; ++k) ff = ff + F[k] * F[k];
+  if constexpr (GD == 2) {
+    J = F[0] * F[3] - F[1] * F[2];
+  } else {
+    J = F[0] * (F[4] * F[8] - F[5] * F[7]) - F[1] * (F[3] * F[8] - F[5] * F[6]) + F[2] * (F[3] * F[7] - F[4] * F[6]);
+  }
+  T lnJ = ad_log(J);
+  return (0.5 * mu) * (ff + (-(double)GD)) - mu * lnJ + (0.5 * lam) * (lnJ * lnJ);
+}
+
+// A[(iJ)(kL)] = d^2 psi / dF_iJ dF_kL by forward-over-forward AD (upper triangle, symmetric fill).
+template <int GD>
+__device__ void neo_tangent_ad(const double (&F)[GD * GD], double lam, double mu, double* __restrict__ A) {
+  constexpr int N = GD * GD;
+  using DD = Dual<Dual<double>>;
+  for (int i = 0; i < N; ++i)
+    for (int j = i; j < N; ++j) {
+      DD x[N];
+#pragma unroll
+      for (int m = 0; m < N; ++m) x[m] = DD{{F[m], m == i ? 1.0 : 0.0}, {m == j ? 1.0 : 0.0, 0.0}};
+      DD r = neo_psi<GD, DD>(x, lam, mu);
+      A[i * N + j] = r.d.d;
+      A[j * N + i] = r.d.d;
+    }
+}
+
+// F at a quadrature point from the cell's nodal displacements and physical gradients.
+template <int GD>
+__device__ __forceinline__ void deformation_gradient(const double* __restrict__ u, const int32_t* cn, int nn,
+                                                     const double* dphi_q, const double (&Ji)[GD][GD],
+                                                     double (&F)[GD * GD]) {
+#pragma unroll
+  for (int i = 0; i < GD; ++i)
+#pragma unroll
+    for (int k = 0; k < GD; ++k) F[i * GD + k] = (i == k) ? 1.0 : 0.0;
+  for (int b = 0; b < nn; ++b) {
+    double gb[GD];
+    phys_grad<GD>(dphi_q + b * GD, Ji, gb);
+    const int64_t n = cn[b];
+#pragma unroll
+    for (int i = 0; i < GD; ++i) {
+      const double ui = u[n * GD + i];
+#pragma unroll
+      for (int k = 0; k < GD; ++k) F[i * GD + k] += ui * gb[k];
+    }
+  }
+}
+
+// K_ab[i][k] += w sum_{J,L} ga[J] A[(iJ)(kL)] gb[L]
+template <int GD>
+__device__ __forceinline__ void neo_block_add(const double* A, const double (&ga)[GD], const double (&gb)[GD], double w,
+                                              double (&K)[GD][GD]) {
+  constexpr int N = GD * GD;
+#pragma unroll
+  for (int i = 0; i < GD; ++i)
+#pragma unroll
+    for (int k = 0; k < GD; ++k) {
+      double sacc = 0.0;
+#pragma unroll
+      for (int J = 0; J < GD; ++J) {
+        double t = 0.0;
+#pragma unroll
+        for (int L = 0; L < GD; ++L) t += A[(i * GD + J) * N + k * GD + L] * gb[L];
+        sacc += ga[J] * t;
+      }
+      K[i][k] += w * sacc;
+    }
+}
+
 // ------------------------------------------------------------------------------------ generic per-block kernel
 // One thread per (cell, a, b). MODE 0: write the cell matrix Ae[c][a*bs+i][b*bs+j].
 // MODE 1: FP64-atomic add into BSR (bc rows/cols skipped); error flag on a missing slot.
@@ -406,6 +527,25 @@ __global__ __launch_bounds__(256) void k_cell_blocks(MeshView M, FormView F, Dev
         damage_cell(M, F, c, g, w, H);
         double ga[2] = {g[a][0], g[a][1]}, gb[2] = {g[b][0], g[b][1]};
         damage_block(ga, gb, w, H, K);
+      }
+    } else if (F.kind == FA_NEO_HOOKEAN) {
+      double lam, mu;
+      cell_lame(F, c, lam, mu);
+#pragma unroll
+      for (int i = 0; i < GD; ++i)
+#pragma unroll
+        for (int j = 0; j < GD; ++j) K[i][j] = 0.0;
+      const int32_t* cn = M.cells + c * nn;
+      for (int q = 0; q < T.nq; ++q) {
+        double Ji[GD][GD];
+        const double wd = T.wq[q] * cell_geometry_q<GD, NV>(M, c, T.gdphi + (size_t)q * NV * GD, Ji);
+        double Fq[GD * GD], A[GD * GD * GD * GD];
+        deformation_gradient<GD>(F.u, cn, nn, T.dphi + (size_t)q * nn * GD, Ji, Fq);
+        neo_tangent_ad<GD>(Fq, lam, mu, A);
+        double ga[GD], gb[GD];
+        phys_grad<GD>(T.dphi + ((size_t)q * nn + a) * GD, Ji, ga);
+        phys_grad<GD>(T.dphi + ((size_t)q * nn + b) * GD, Ji, gb);
+        neo_block_add<GD>(A, ga, gb, wd, K);
       }
     } else {
       double lam, mu;
@@ -514,11 +654,19 @@ static constexpr int kGatherMaxRows = 128;      // rows per chunk
 template <int GD, int NV, int NQ, int MAT>
 struct Rec {
   static constexpr bool SIMP = (NV == GD + 1);
+  static constexpr int N = GD * GD;
+  static constexpr int NTRI = N * (N + 1) / 2;  // stored upper triangle of the tangent
   // LIN simplex: Ji[GD*GD], wdet, lam, mu | LIN tensor: NQ x (Ji[GD*GD], wdet), lam, mu |
-  // DAMAGE (P1 tri): g[3][2], w, H[3][3]
-  static constexpr int RAW = MAT == FA_ASYM_DAMAGE ? 16 : (SIMP ? GD * GD + 3 : NQ * (GD * GD + 1) + 2);
+  // DAMAGE (P1 tri): g[3][2], w, H[3][3] | NEO (simplex): Ji[GD*GD], wdet, NQ x A_q upper triangle
+  static constexpr int RAW = MAT == FA_ASYM_DAMAGE ? 16
+                             : MAT == FA_NEO_HOOKEAN ? N + 1 + NQ * NTRI
+                                                     : (SIMP ? GD * GD + 3 : NQ * (GD * GD + 1) + 2);
   static constexpr int SIZE = (RAW + 1) & ~1;  // even: 16-byte aligned records
 };
+
+__host__ __device__ constexpr int tri_index(int i, int j, int n) {  // upper triangle, i <= j
+  return i * n - i * (i - 1) / 2 + (j - i);
+}
 
 struct GatherArgs {
   MeshView M;
@@ -543,6 +691,33 @@ __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, co
                                                       uint32_t* __restrict__ bcmask) {
   using R = Rec<GD, NV, NQ, MAT>;
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < M.ncells; c += (int64_t)gridDim.x * blockDim.x) {
+  if constexpr (MAT == FA_NEO_HOOKEAN) {
+    static_assert(R::SIMP, "neo-Hookean gather records: affine simplices");
+    constexpr int N = R::N;
+    double* out = rec + c * R::SIZE;
+    double Ji[GD][GD];
+    const double det = fabs(simplex_geometry<GD>(M, c, Ji));
+#pragma unroll
+    for (int i = 0; i < GD; ++i)
+#pragma unroll
+      for (int k = 0; k < GD; ++k) out[i * GD + k] = Ji[i][k];
+    out[N] = det;
+    double lam, mu;
+    cell_lame(F, c, lam, mu);
+    const int32_t* cn = M.cells + c * NN;
+    for (int q = 0; q < NQ; ++q) {
+      double Fq[N];
+      deformation_gradient<GD>(F.u, cn, NN, tab + NQ + q * NN * GD, Ji, Fq);
+      using DD = Dual<Dual<double>>;
+      for (int i = 0; i < N; ++i)
+        for (int j = i; j < N; ++j) {
+          DD x[N];
+#pragma unroll
+          for (int m = 0; m < N; ++m) x[m] = DD{{Fq[m], m == i ? 1.0 : 0.0}, {m == j ? 1.0 : 0.0, 0.0}};
+          out[N + 1 + q * R::NTRI + tri_index(i, j, N)] = neo_psi<GD, DD>(x, lam, mu).d.d;
+        }
+    }
+  } else {
   double r[R::SIZE];
 #pragma unroll
   for (int k = 0; k < R::SIZE; ++k) r[k] = 0.0;
@@ -594,6 +769,7 @@ __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, co
   double2* out = reinterpret_cast<double2*>(rec + c * R::SIZE);
 #pragma unroll
   for (int k = 0; k < R::SIZE / 2; ++k) out[k] = make_double2(r[2 * k], r[2 * k + 1]);
+  }
   if (bcmask) {
     uint32_t m = 0;
     const int32_t* cn = M.cells + c * NN;
@@ -640,8 +816,9 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   __shared__ int32_t cols[MAXB];
   __shared__ int32_t rowoff[kGatherMaxRows + 1];
   __shared__ uint8_t adjrow[kGatherMaxAdj];
-  __shared__ double s_w[SIMP ? 1 : NQ];
-  __shared__ double s_dphi[SIMP ? 1 : NQ * NN * GD];
+  constexpr bool NEO = (MAT == FA_NEO_HOOKEAN);
+  __shared__ double s_w[SIMP && !NEO ? 1 : NQ];
+  __shared__ double s_dphi[SIMP && !NEO ? 1 : NQ * NN * GD];
   __shared__ double s_ahat[SIMP ? NN * NN * BS2 : 1];
 
   // XCD-aware chunk order: blocks b and b+8 share an XCD (round-robin dispatch), so XCD
@@ -667,7 +844,10 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     int64_t j0 = P.adj_ptr[r0 + t], j1 = P.adj_ptr[r0 + t + 1];
     for (int64_t j = j0; j < j1; ++j) adjrow[j - a0] = (uint8_t)t;
   }
-  if constexpr (SIMP) {
+  if constexpr (NEO) {
+    for (int t = tid; t < NQ; t += 256) s_w[t] = P.tab[t];
+    for (int t = tid; t < NQ * NN * GD; t += 256) s_dphi[t] = P.tab[NQ + t];
+  } else if constexpr (SIMP) {
     for (int t = tid; t < NN * NN * BS2; t += 256) s_ahat[t] = P.ahat[t];
   } else {
     for (int t = tid; t < NQ; t += 256) s_w[t] = P.tab[t];
@@ -684,10 +864,11 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     const int lr = adjrow[j];
     const int lo = rowoff[lr], hi = rowoff[lr + 1];
     // one record + the column nodes + the bc mask: all independent loads, issued together
-    double r[R::SIZE];
+    constexpr int RL = NEO ? ((BS2 + 2) & ~1) : R::SIZE;  // registers: NEO keeps only Ji, wdet
+    double r[RL];
     const double2* rp = reinterpret_cast<const double2*>(P.rec + c * R::SIZE);
 #pragma unroll
-    for (int k = 0; k < R::SIZE / 2; ++k) {
+    for (int k = 0; k < RL / 2; ++k) {
       double2 v = rp[k];
       r[2 * k] = v.x;
       r[2 * k + 1] = v.y;
@@ -723,6 +904,65 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
           for (int jj = 0; jj < 2; ++jj)
             if (!((mask >> (aloc * 2 + i)) & 1u) && !((mask >> (b * 2 + jj)) & 1u))
               atomicAdd(&acc[s * 4 + i * 2 + jj], K[i][jj]);
+      }
+    } else if constexpr (NEO) {
+      constexpr int N = R::N;
+      const double* Aq0 = P.rec + c * R::SIZE + N + 1;
+      const double wdet = r[BS2];
+      double ga[NQ][GD];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int d = 0; d < GD; ++d) {
+          double sgd = 0.0;
+#pragma unroll
+          for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + aloc) * GD + k] * r[k * GD + d];
+          ga[q][d] = s_w[q] * wdet * sgd;
+        }
+#pragma unroll FA_GATHER_UNROLL_B
+      for (int bb = 0; bb < NBG; ++bb) {
+        const int b = part * NBG + bb;
+        if (b >= NN) break;
+        double K[GD][GD];
+#pragma unroll
+        for (int i = 0; i < GD; ++i)
+#pragma unroll
+          for (int k = 0; k < GD; ++k) K[i][k] = 0.0;
+        for (int q = 0; q < NQ; ++q) {
+          double gb[GD];
+#pragma unroll
+          for (int d = 0; d < GD; ++d) {
+            double sgd = 0.0;
+#pragma unroll
+            for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + b) * GD + k] * r[k * GD + d];
+            gb[d] = sgd;
+          }
+          const double* Aq = Aq0 + q * R::NTRI;
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int J = 0; J < GD; ++J) {
+              const int row = i * GD + J;
+#pragma unroll
+              for (int k = 0; k < GD; ++k) {
+                double t = 0.0;
+#pragma unroll
+                for (int L = 0; L < GD; ++L) {
+                  const int col = k * GD + L;
+                  t += Aq[row <= col ? tri_index(row, col, N) : tri_index(col, row, N)] * gb[L];
+                }
+                K[i][k] += ga[q][J] * t;
+              }
+            }
+        }
+        const int s = lds_find(cols, lo, hi, cn[bb]);
+        if (s < 0) { atomicOr(P.err, 1); continue; }
+#pragma unroll
+        for (int i = 0; i < GD; ++i)
+#pragma unroll
+          for (int jj = 0; jj < GD; ++jj)
+            if (!((mask >> (aloc * GD + i)) & 1u) && !((mask >> (b * GD + jj)) & 1u))
+              atomicAdd(&acc[s * BS2 + i * GD + jj], K[i][jj]);
       }
     } else if constexpr (SIMP) {
       // affine simplex: G_ab = |J| Ji^T Ahat_ab Ji  (reference-tensor form)
@@ -1083,6 +1323,8 @@ static int form_view(const fa_mesh* mesh, const fa_form* form, FormView& F) {
   if (F.kind == FA_ASYM_DAMAGE) {
     if (mesh->cell_type != FA_TRIANGLE || mesh->degree != 1)
       return fail(FA_E_UNSUPPORTED, "FA_ASYM_DAMAGE is the reference's 2-D P1-triangle law");
+  } else if (F.kind == FA_NEO_HOOKEAN) {
+    if (!F.u) return fail(FA_E_ARG, "FA_NEO_HOOKEAN needs the state u");
   } else if (F.kind != FA_LINEAR_ELASTICITY) {
     return fail(FA_E_UNSUPPORTED, "form kind %d not implemented", F.kind);
   }
@@ -1140,6 +1382,14 @@ static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const
   *handled = true;
   const int ct = m->cell_type, p = m->degree, nq = T.nq;
   if (kind == FA_ASYM_DAMAGE) return launch_gather<2, 3, 3, 1, 1, FA_ASYM_DAMAGE>(P, bc, s);
+  if (kind == FA_NEO_HOOKEAN) {
+    if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, 5, FA_NEO_HOOKEAN>(P, bc, s);
+    if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, FA_NEO_HOOKEAN>(P, bc, s);
+    if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, FA_NEO_HOOKEAN>(P, bc, s);
+    if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, FA_NEO_HOOKEAN>(P, bc, s);
+    *handled = false;
+    return FA_OK;
+  }
   if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, 0>(P, bc, s);
   if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, 0>(P, bc, s);
   if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, 0>(P, bc, s);
@@ -1290,23 +1540,6 @@ __device__ __forceinline__ void damage_stress(double s00, double s11, double s01
     sig[0][0] = m2plw * s00 + lw * s11;
     sig[1][1] = m2plw * s11 + lw * s00;
     sig[0][1] = sig[1][0] = w * m * (s01 + s01);
-  }
-}
-
-// geometry at quadrature point q of cell c: Jinv and |det J| (affine simplex: constant)
-template <int GD, int NV>
-__device__ __forceinline__ double cell_geometry_q(const MeshView& M, int64_t c, const double* gdphi_q,
-                                                  double (&Ji)[GD][GD]) {
-  if constexpr (NV == GD + 1) {
-    return fabs(simplex_geometry<GD>(M, c, Ji));
-  } else {
-    double xv[NV][GD];
-    const int32_t* gv = M.geom + c * NV;
-#pragma unroll
-    for (int v = 0; v < NV; ++v)
-#pragma unroll
-      for (int i = 0; i < GD; ++i) xv[v][i] = M.x[(int64_t)gv[v] * GD + i];
-    return fabs(tensor_geometry<GD, NV>(xv, gdphi_q, Ji));
   }
 }
 

@@ -397,6 +397,19 @@ class AsymDamage(LinearElasticity):
         self.d = None if d is None else (d.x if isinstance(d, Function) else d)
 
 
+class NeoHookean(LinearElasticity):
+    """Compressible neo-Hookean tangent (BASELINE config E): psi = mu/2 (I_C - 3) - mu ln J +
+    lmbda/2 (ln J)^2, F = I + grad u; J = derivative of the first Piola stress, taken on the
+    GPU by forward-over-forward automatic differentiation of psi (the pattern of the reference's
+    MFEM AD, MFEM/mechanic2d/autodiff/admfem.hpp:672-700). u: the state (required)."""
+    kind = _lib.FA_NEO_HOOKEAN
+
+    def __init__(self, V: FunctionSpace, E=None, nu=0.3, u=None, lam=None, mu=None, quadrature_degree=None, f=None):
+        if u is None:
+            raise ValueError("NeoHookean needs the state u")
+        super().__init__(V, E=E, nu=nu, lam=lam, mu=mu, quadrature_degree=quadrature_degree, u=u, f=f)
+
+
 def _cellwise(v, nc, dev):
     if isinstance(v, Function):
         v = v.x

@@ -883,3 +883,126 @@ int ora_apply_lifting(const ora_mesh* M, int kind, const double* lam, const doub
   free(Ae); free(dphi); free(gdphi);
   return 0;
 }
+
+/* ---------------------------------------------------------------- neo-Hookean (config E) */
+/* psi(F) = mu/2 (I_C - 3) - mu ln J + lam/2 (ln J)^2 (2-D: plane strain). Closed-form tangent
+ * (independent of the device's AD): with G = F^{-1},
+ * A[(iJ)(kL)] = mu d_ik d_JL + (mu - lam ln J) G_Jk G_Li + lam G_Ji G_Lk. */
+static void neo_tangent(int gd, const double* F, double lam, double mu, double* A) {
+  double G[9], J;
+  if (gd == 2) {
+    J = F[0] * F[3] - F[1] * F[2];
+    G[0] = F[3] / J; G[1] = -F[1] / J; G[2] = -F[2] / J; G[3] = F[0] / J;
+  } else {
+    double Jm[9];
+    for (int k = 0; k < 9; ++k) Jm[k] = F[k];
+    double Ji[9];
+    /* reuse the geometry inverse: jacobian() builds J from vertices, so invert directly */
+    J = Jm[0] * (Jm[4] * Jm[8] - Jm[5] * Jm[7]) - Jm[1] * (Jm[3] * Jm[8] - Jm[5] * Jm[6]) +
+        Jm[2] * (Jm[3] * Jm[7] - Jm[4] * Jm[6]);
+    Ji[0] = (Jm[4] * Jm[8] - Jm[5] * Jm[7]) / J;
+    Ji[1] = (Jm[2] * Jm[7] - Jm[1] * Jm[8]) / J;
+    Ji[2] = (Jm[1] * Jm[5] - Jm[2] * Jm[4]) / J;
+    Ji[3] = (Jm[5] * Jm[6] - Jm[3] * Jm[8]) / J;
+    Ji[4] = (Jm[0] * Jm[8] - Jm[2] * Jm[6]) / J;
+    Ji[5] = (Jm[2] * Jm[3] - Jm[0] * Jm[5]) / J;
+    Ji[6] = (Jm[3] * Jm[7] - Jm[4] * Jm[6]) / J;
+    Ji[7] = (Jm[1] * Jm[6] - Jm[0] * Jm[7]) / J;
+    Ji[8] = (Jm[0] * Jm[4] - Jm[1] * Jm[3]) / J;
+    for (int k = 0; k < 9; ++k) G[k] = Ji[k];
+  }
+  double lnJ = log(J);
+  int N = gd * gd;
+  for (int i = 0; i < gd; ++i)
+    for (int Jx = 0; Jx < gd; ++Jx)
+      for (int k = 0; k < gd; ++k)
+        for (int L = 0; L < gd; ++L)
+          A[(i * gd + Jx) * N + k * gd + L] = ((i == k && Jx == L) ? mu : 0.0) +
+                                              (mu - lam * lnJ) * G[Jx * gd + k] * G[L * gd + i] +
+                                              lam * G[Jx * gd + i] * G[L * gd + k];
+}
+
+/* K[(a,i),(b,k)] += sum_q w|J| sum_{J,L} g_a[J] A_q[(iJ)(kL)] g_b[L], F_q = I + sum_b u_b (x) g_b(q) */
+static void neo_cell(int gd, int nn, int nq, const double* wq, const double* dphi, int nv, const double* gdphi,
+                     const double* xv, const double* uc, double lam, double mu, double* Ae) {
+  int nd = nn * gd, N = gd * gd;
+  double Jinv[9], g[ORA_MAXN * 3], F[9], A[81];
+  for (int q = 0; q < nq; ++q) {
+    double det = jacobian(gd, nv, &gdphi[q * nv * gd], xv, Jinv);
+    double w = wq[q] * fabs(det);
+    phys_grads(gd, nn, &dphi[q * nn * gd], Jinv, g);
+    for (int i = 0; i < gd; ++i)
+      for (int k = 0; k < gd; ++k) {
+        double s = (i == k) ? 1.0 : 0.0;
+        for (int b = 0; b < nn; ++b) s += uc[b * gd + i] * g[b * gd + k];
+        F[i * gd + k] = s;
+      }
+    neo_tangent(gd, F, lam, mu, A);
+    for (int a = 0; a < nn; ++a)
+      for (int b = 0; b < nn; ++b)
+        for (int i = 0; i < gd; ++i)
+          for (int k = 0; k < gd; ++k) {
+            double s = 0;
+            for (int Jx = 0; Jx < gd; ++Jx)
+              for (int L = 0; L < gd; ++L) s += g[a * gd + Jx] * A[(i * gd + Jx) * N + k * gd + L] * g[b * gd + L];
+            Ae[(a * gd + i) * nd + b * gd + k] += w * s;
+          }
+  }
+}
+
+/* neo-Hookean tangent assembly (dolfinx semantics, as ora_assemble_elasticity); also returns the
+ * cell matrices when Aout != NULL (then indptr/indices/values may be NULL). */
+int ora_assemble_neohookean(const ora_mesh* M, const double* lam, const double* mu, const double* u, int qdeg,
+                            const int8_t* bc, double diag, const int64_t* indptr, const int32_t* indices,
+                            double* values, double* Aout) {
+  int gd = M->gdim, nn = M->nn, nv = M->nv, bs = gd, nd = nn * gd;
+  if (qdeg < 0) qdeg = simplex(M->cell_type) ? 2 * (M->degree - 1) : 2 * M->degree;
+  static double pts[ORA_MAXQ * 3], wq[ORA_MAXQ];
+  int nq = ora_quadrature(M->cell_type, qdeg, pts, wq);
+  double* dphi = (double*)malloc(sizeof(double) * nq * nn * gd);
+  double* gdphi = (double*)malloc(sizeof(double) * nq * nv * gd);
+  ora_tabulate(M->cell_type, M->degree, nq, pts, NULL, dphi);
+  ora_tabulate(M->cell_type, 1, nq, pts, NULL, gdphi);
+  double* Ae = (double*)malloc(sizeof(double) * nd * nd);
+  double xv[8 * 3], uc[ORA_MAXN * 3];
+  for (int64_t c = 0; c < M->ncells; ++c) {
+    const int32_t* nodes = &M->cells[c * nn];
+    memset(Ae, 0, sizeof(double) * nd * nd);
+    for (int v = 0; v < nv; ++v)
+      for (int d = 0; d < gd; ++d) xv[v * gd + d] = M->x[(int64_t)M->geom[c * nv + v] * gd + d];
+    for (int a = 0; a < nn; ++a)
+      for (int d = 0; d < gd; ++d) uc[a * gd + d] = u[(int64_t)nodes[a] * gd + d];
+    neo_cell(gd, nn, nq, wq, dphi, nv, gdphi, xv, uc, lam[c], mu[c], Ae);
+    if (Aout) {
+      memcpy(&Aout[c * nd * nd], Ae, sizeof(double) * nd * nd);
+      continue;
+    }
+    if (bc)
+      for (int i = 0; i < nd; ++i)
+        if (bc[(int64_t)nodes[i / bs] * bs + i % bs])
+          for (int j = 0; j < nd; ++j) Ae[i * nd + j] = Ae[j * nd + i] = 0.0;
+    for (int a = 0; a < nn; ++a)
+      for (int b = 0; b < nn; ++b) {
+        int64_t s = find_col(indptr, indices, nodes[a], nodes[b]);
+        if (s < 0) { free(Ae); free(dphi); free(gdphi); return -4; }
+        for (int i = 0; i < bs; ++i)
+          for (int j = 0; j < bs; ++j) values[s * bs * bs + i * bs + j] += Ae[(a * bs + i) * nd + b * bs + j];
+      }
+  }
+  free(Ae); free(dphi); free(gdphi);
+  if (bc && !Aout) {
+    int64_t nnodes = 0;
+    for (int64_t c = 0; c < M->ncells * nn; ++c)
+      if (M->cells[c] + 1 > nnodes) nnodes = M->cells[c] + 1;
+    for (int64_t r = 0; r < nnodes; ++r)
+      for (int i = 0; i < bs; ++i)
+        if (bc[r * bs + i]) {
+          int64_t s = find_col(indptr, indices, r, (int32_t)r);
+          if (s >= 0) values[s * bs * bs + i * bs + i] = diag;
+        }
+  }
+  return 0;
+}
+
+/* public wrapper for tests */
+void ora_neo_tangent(int gd, const double* F, double lam, double mu, double* A) { neo_tangent(gd, F, lam, mu, A); }

@@ -62,6 +62,9 @@ def lib():
         L.ora_assemble_elasticity.argtypes = [ctypes.POINTER(_Mesh), P, P, ctypes.c_int, P, ctypes.c_double, P, P, P]
         L.ora_assemble_damage.argtypes = [ctypes.POINTER(_Mesh), P, P, P, P, P, ctypes.c_double, P, P, P]
         L.ora_cell_matrices_elasticity.argtypes = [ctypes.POINTER(_Mesh), P, P, ctypes.c_int, P]
+        L.ora_assemble_neohookean.argtypes = [ctypes.POINTER(_Mesh), P, P, P, ctypes.c_int, P, ctypes.c_double, P,
+                                              P, P, P]
+        L.ora_neo_tangent.argtypes = [ctypes.c_int, P, ctypes.c_double, ctypes.c_double, P]
         L.ora_assemble_residual.argtypes = [ctypes.POINTER(_Mesh), ctypes.c_int, P, P, P, P, P, ctypes.c_int, P]
         L.ora_apply_lifting.argtypes = [ctypes.POINTER(_Mesh), ctypes.c_int, P, P, P, P, ctypes.c_int, P, P, P,
                                         ctypes.c_double, P]
@@ -262,3 +265,40 @@ def apply_lifting(cell_type, degree, cells, geom, x, lam, mu, b, bc, g, x0=None,
                                 alpha, _p(b))
     assert r == 0
     return b
+
+
+def assemble_neohookean(cell_type, degree, cells, geom, x, lam, mu, u, indptr=None, indices=None, bc=None, diag=1.0,
+                        qdeg=-1, cell_matrices=False):
+    """neo-Hookean tangent (closed form) assembled with dolfinx semantics, or the cell matrices."""
+    cells = np.ascontiguousarray(cells, dtype=np.int32)
+    geom = np.ascontiguousarray(geom, dtype=np.int32)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    nc, nn = cells.shape
+    lam = np.ascontiguousarray(np.broadcast_to(lam, (nc,)), dtype=np.float64)
+    mu = np.ascontiguousarray(np.broadcast_to(mu, (nc,)), dtype=np.float64)
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    bs = _GDIM[cell_type]
+    m = _mesh_struct(cell_type, degree, cells, geom, x)
+    if cell_matrices:
+        A = np.zeros((nc, nn * bs, nn * bs))
+        r = lib().ora_assemble_neohookean(ctypes.byref(m), _p(lam), _p(mu), _p(u), qdeg, None, diag, None, None, None,
+                                          _p(A))
+        assert r == 0
+        return A
+    vals = np.zeros((indices.shape[0], bs, bs))
+    bcp = None
+    if bc is not None:
+        bc = np.ascontiguousarray(bc, dtype=np.int8)
+        bcp = _p(bc)
+    r = lib().ora_assemble_neohookean(ctypes.byref(m), _p(lam), _p(mu), _p(u), qdeg, bcp, diag, _p(indptr),
+                                      _p(indices), _p(vals), None)
+    assert r == 0, r
+    return vals
+
+
+def neo_tangent(F, lam, mu):
+    F = np.ascontiguousarray(F, dtype=np.float64)
+    gd = F.shape[0]
+    A = np.zeros((gd * gd, gd * gd))
+    lib().ora_neo_tangent(gd, _p(F), lam, mu, _p(A))
+    return A

@@ -1,0 +1,77 @@
+"""GPU parity of the neo-Hookean tangent (BASELINE config E): device forward-over-forward AD vs the
+oracle's closed-form tangent, through gather, scatter and the per-cell tabulation."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+def _setup(oracle, ct, p, n, dev, amp=0.05):
+    from femasm import fem, mesh
+
+    m = mesh.create_unit_square(*n, cell_type=ct, device=dev) if len(n) == 2 else \
+        mesh.create_unit_cube(*n, cell_type=ct, device=dev)
+    V = fem.functionspace(m, ("Lagrange", p, (m.gdim,)))
+    xn = V.tabulate_dof_coordinates()
+    # u = amp * (sin pi x, sin pi y[, sin pi z]) at the nodes (SURVEY §8d neo-Hookean state)
+    u = (amp * torch.sin(torch.pi * xn)).reshape(-1).contiguous()
+    E = torch.tensor(oracle.e_range()[np.arange(m.num_cells) % 200], device=dev)
+    a = fem.NeoHookean(V, E=E, nu=0.3, u=u)
+    return m, V, a
+
+
+def _np(t):
+    return t.cpu().numpy()
+
+
+CASES = [(3, 1, (5, 4)), (3, 2, (4, 3)), (-4, 1, (2, 3, 2)), (-4, 2, (2, 2, 3)), (4, 2, (3, 2)), (8, 1, (2, 2, 2))]
+
+
+@pytest.mark.parametrize("method", ["gather", "scatter"])
+@pytest.mark.parametrize("ct,p,n", CASES)
+def test_neohookean_matrix(oracle, dev, ct, p, n, method):
+    from femasm import fem
+
+    m, V, a = _setup(oracle, ct, p, n, dev)
+    left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
+    bcs = [fem.dirichletbc(0.0, left, V)]
+    A = fem.assemble_matrix(a, bcs=bcs, method=method)
+    marker, _ = fem._combine_bcs(V, bcs)
+    indptr, indices = oracle.sparsity(_np(V.dofmap), V.num_nodes)
+    lam, mu = oracle.lame(_np(a.E), 0.3)
+    ref = oracle.assemble_neohookean(ct, p, _np(V.dofmap), _np(m.cells), _np(m.x), lam, mu, _np(a.u), indptr, indices,
+                                     bc=_np(marker))
+    assert np.abs(_np(A.data) - ref).max() <= RTOL * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("ct,p,n", CASES[:4])
+def test_neohookean_cell_matrices(oracle, dev, ct, p, n):
+    from femasm import fem
+
+    m, V, a = _setup(oracle, ct, p, n, dev)
+    Ae = _np(fem.tabulate_cells(a))
+    lam, mu = oracle.lame(_np(a.E), 0.3)
+    ref = oracle.assemble_neohookean(ct, p, _np(V.dofmap), _np(m.cells), _np(m.x), lam, mu, _np(a.u),
+                                     cell_matrices=True)
+    assert np.abs(Ae - ref).max() <= RTOL * np.abs(ref).max()
+
+
+def test_neohookean_reduces_to_linear_at_zero_state(oracle, dev):
+    """At u = 0 (F = I) the neo-Hookean tangent is the linear-elasticity tangent."""
+    from femasm import fem
+
+    m, V, a = _setup(oracle, -4, 2, (2, 2, 2), dev, amp=0.0)
+    A1 = fem.assemble_matrix(a)
+    d1 = A1.data.clone()
+    lin = fem.LinearElasticity(V, E=a.E, nu=0.3)
+    A2 = fem.assemble_matrix(lin)
+    assert ((A2.data - d1).abs().max() <= RTOL * d1.abs().max()).item()

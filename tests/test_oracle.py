@@ -137,3 +137,66 @@ def test_rigid_body_null_space(oracle, ct, p):
     ev = np.linalg.eigvalsh(K)
     assert (ev > -1e-10 * ev.max()).all()
     assert (np.abs(ev) < 1e-10 * ev.max()).sum() == len(modes)
+
+
+def _psi_sympy():
+    """The reference damage potential (FEniCSx/mechanic2d/asym_ufl.py:37-51 = MFEM Potential,
+    MFEM/mechanic2d/asym_elasto_damage_model.cc:100-155) in Voigt strains (e00, e11, gamma=2 e01),
+    with the indicator alphas as symbols (piecewise constant where the signs do not change)."""
+    e00, e11, gam, lam, mu, d, al, al1, al2 = sp.symbols("e00 e11 gamma lam mu d al al1 al2", real=True)
+    e01 = gam / 2
+    I1 = e00 + e11
+    I2 = e01 * e01 - e00 * e11
+    r = sp.sqrt(I1 * I1 + 4 * I2)
+    ev1, ev2 = (I1 + r) / 2, (I1 - r) / 2
+    psi = I1 * I1 * (1 - al * d) * lam / 2 + mu * ((1 - al1 * d) * ev1 ** 2 + (1 - al2 * d) * ev2 ** 2)
+    return psi, (e00, e11, gam), (lam, mu, d, al, al1, al2), (ev1, ev2, I1)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_damage_tangent_is_hessian_of_reference_potential(oracle, seed):
+    """MFEM's hand-written tangent `hook` (restated in the oracle) equals the SymPy Hessian of the
+    UFL potential psi; asym_stress equals its gradient. Pins rows a2-a4 of SURVEY §8."""
+    psi, evars, pvars, (ev1, ev2, I1) = _psi_sympy()
+    grad = [sp.diff(psi, v) for v in evars]
+    hess = [[sp.diff(g, v) for v in evars] for g in grad]
+    rng = np.random.default_rng(seed)
+    lam, mu = 5.7e7, 3.8e7
+    d = float(rng.uniform(0.05, 0.95))
+    s = rng.normal(size=3) * 1e-3
+    strain = np.array([s[0], s[1], s[2]])  # e00, e11, e01
+    sub = {evars[0]: strain[0], evars[1]: strain[1], evars[2]: 2 * strain[2], pvars[0]: lam, pvars[1]: mu,
+           pvars[2]: d}
+    e1v, e2v, i1v = [float(x.subs(sub)) for x in (ev1, ev2, I1)]
+    sub.update({pvars[3]: 1.0 if i1v >= 0 else 0.0, pvars[4]: 1.0 if e1v >= 0 else 0.0,
+                pvars[5]: 1.0 if e2v >= 0 else 0.0})
+    H = np.array([[float(h.subs(sub)) for h in row] for row in hess])
+    G = np.array([float(g.subs(sub)) for g in grad])
+    hook = oracle.damage_hook(strain, lam, mu, d)
+    np.testing.assert_allclose(hook, H, rtol=1e-9, atol=1e-9 * np.abs(H).max())
+    sig = oracle.damage_stress(strain, lam, mu, d, w=1.0)  # (s00, s11, s01)
+    np.testing.assert_allclose(sig, G, rtol=1e-9, atol=1e-9 * np.abs(G).max())
+
+
+def test_damage_law_linear_limit(oracle):
+    """d = 0 gives the linear Hooke tangent (the bridge from the reference to the linear configs)."""
+    lam, mu = 2.0, 1.5
+    h = oracle.damage_hook(np.array([1e-3, -2e-3, 5e-4]), lam, mu, 0.0)
+    np.testing.assert_array_equal(h, [[lam + 2 * mu, lam, 0], [lam, lam + 2 * mu, 0], [0, 0, mu]])
+
+
+@pytest.mark.parametrize("gd", [2, 3])
+def test_neo_hookean_tangent_is_hessian(oracle, gd):
+    """The oracle's closed-form neo-Hookean tangent equals the SymPy Hessian of psi(F)."""
+    Fs = sp.Matrix(gd, gd, lambda i, j: sp.Symbol(f"F{i}{j}", real=True))
+    lam, mu = sp.Rational(17, 10), sp.Rational(9, 10)
+    J = Fs.det()
+    psi = mu / 2 * (sum(v ** 2 for v in Fs) + (1 if gd == 2 else 0) - 3) - mu * sp.log(J) + lam / 2 * sp.log(J) ** 2
+    flat = list(Fs)
+    H = sp.hessian(psi, flat)
+    rng = np.random.default_rng(gd)
+    Fn = np.eye(gd) + 0.1 * rng.uniform(-1, 1, (gd, gd))
+    sub = {flat[k]: Fn.reshape(-1)[k] for k in range(gd * gd)}
+    Hn = np.array(H.subs(sub).evalf(30).tolist(), dtype=np.float64)
+    A = oracle.neo_tangent(Fn, 1.7, 0.9)
+    np.testing.assert_allclose(A, Hn, rtol=1e-12, atol=1e-12)
