@@ -50,6 +50,8 @@ CONFIGS = {
     "D": dict(cell="hexahedron", degree=3, n=58, qdeg=None, label="3-D Q3 hex, 58^3 (192x192 local)"),
     "Dq2": dict(cell="hexahedron", degree=2, n=58, qdeg=None, label="3-D Q2 hex, 58^3 (81x81 local)"),
     "E": dict(cell="tetrahedron", degree=2, n=203, qdeg=None, label="3-D P2 tet, 203^3x6 (config E mesh)"),
+    "Eneo": dict(cell="tetrahedron", degree=2, n=203, qdeg=2, form="neo",
+                 label="3-D P2 tet neo-Hookean (AD tangent), 203^3x6, u = 1e-3 sin(pi x)"),
 }
 
 
@@ -82,7 +84,12 @@ def build_problem(n, dev, z_range=None, cfg=None):
     ncell_global0 = (z_range[0] if z_range else 0) * per_layer
     cid = torch.arange(m.num_cells, device=dev, dtype=torch.int64) + ncell_global0
     E = torch.tensor(e_range(), dtype=torch.float64, device=dev)[cid % 200]
-    a = fem.form(fem.LinearElasticity(V, E=E, nu=0.3, quadrature_degree=cfg["qdeg"]))
+    if cfg.get("form") == "neo":
+        # SURVEY §8d neo-Hookean state: u = 1e-3 (sin pi x, sin pi y, sin pi z) at the nodes
+        u = (1e-3 * torch.sin(torch.pi * V.tabulate_dof_coordinates())).reshape(-1).contiguous()
+        a = fem.form(fem.NeoHookean(V, E=E, nu=0.3, u=u, quadrature_degree=cfg["qdeg"]))
+    else:
+        a = fem.form(fem.LinearElasticity(V, E=E, nu=0.3, quadrature_degree=cfg["qdeg"]))
     left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
     right = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.ones_like(x[0])))
     bcs = [fem.dirichletbc(0.0, left, V), fem.dirichletbc([0.01] + [0.0] * (gd - 1), right, V)]

@@ -906,29 +906,49 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
               atomicAdd(&acc[s * 4 + i * 2 + jj], K[i][jj]);
       }
     } else if constexpr (NEO) {
+      // K_ab[i][k] = sum_q w_q |J| sum_{J,L} ga_q[J] A_q[(iJ)(kL)] gb_q[L]; per q the row node's
+      // gradient is contracted first, C[i][k][L] = sum_J ga[J] A[(iJ)(kL)] (compile-time indices,
+      // each tangent entry loaded once per item), then applied to every column node.
       constexpr int N = R::N;
       const double* Aq0 = P.rec + c * R::SIZE + N + 1;
       const double wdet = r[BS2];
-      double ga[NQ][GD];
+      double K[NBG][GD][GD];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q)
+      for (int bb = 0; bb < NBG; ++bb)
+#pragma unroll
+        for (int i = 0; i < GD; ++i)
+#pragma unroll
+          for (int k = 0; k < GD; ++k) K[bb][i][k] = 0.0;
+#pragma unroll 1
+      for (int q = 0; q < NQ; ++q) {
+        double ga[GD];
 #pragma unroll
         for (int d = 0; d < GD; ++d) {
           double sgd = 0.0;
 #pragma unroll
           for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + aloc) * GD + k] * r[k * GD + d];
-          ga[q][d] = s_w[q] * wdet * sgd;
+          ga[d] = s_w[q] * wdet * sgd;
         }
-#pragma unroll FA_GATHER_UNROLL_B
-      for (int bb = 0; bb < NBG; ++bb) {
-        const int b = part * NBG + bb;
-        if (b >= NN) break;
-        double K[GD][GD];
+        const double* Aq = Aq0 + q * R::NTRI;
+        double C[GD][GD][GD];
 #pragma unroll
         for (int i = 0; i < GD; ++i)
 #pragma unroll
-          for (int k = 0; k < GD; ++k) K[i][k] = 0.0;
-        for (int q = 0; q < NQ; ++q) {
+          for (int k = 0; k < GD; ++k)
+#pragma unroll
+            for (int L = 0; L < GD; ++L) {
+              double t = 0.0;
+#pragma unroll
+              for (int J = 0; J < GD; ++J) {
+                const int row = i * GD + J, col = k * GD + L;
+                t += ga[J] * Aq[row <= col ? tri_index(row, col, N) : tri_index(col, row, N)];
+              }
+              C[i][k][L] = t;
+            }
+#pragma unroll
+        for (int bb = 0; bb < NBG; ++bb) {
+          const int b = part * NBG + bb;
+          if (b >= NN) break;
           double gb[GD];
 #pragma unroll
           for (int d = 0; d < GD; ++d) {
@@ -937,24 +957,21 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
             for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + b) * GD + k] * r[k * GD + d];
             gb[d] = sgd;
           }
-          const double* Aq = Aq0 + q * R::NTRI;
 #pragma unroll
           for (int i = 0; i < GD; ++i)
 #pragma unroll
-            for (int J = 0; J < GD; ++J) {
-              const int row = i * GD + J;
+            for (int k = 0; k < GD; ++k) {
+              double t = 0.0;
 #pragma unroll
-              for (int k = 0; k < GD; ++k) {
-                double t = 0.0;
-#pragma unroll
-                for (int L = 0; L < GD; ++L) {
-                  const int col = k * GD + L;
-                  t += Aq[row <= col ? tri_index(row, col, N) : tri_index(col, row, N)] * gb[L];
-                }
-                K[i][k] += ga[q][J] * t;
-              }
+              for (int L = 0; L < GD; ++L) t += C[i][k][L] * gb[L];
+              K[bb][i][k] += t;
             }
         }
+      }
+#pragma unroll
+      for (int bb = 0; bb < NBG; ++bb) {
+        const int b = part * NBG + bb;
+        if (b >= NN) break;
         const int s = lds_find(cols, lo, hi, cn[bb]);
         if (s < 0) { atomicOr(P.err, 1); continue; }
 #pragma unroll
@@ -962,7 +979,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
 #pragma unroll
           for (int jj = 0; jj < GD; ++jj)
             if (!((mask >> (aloc * GD + i)) & 1u) && !((mask >> (b * GD + jj)) & 1u))
-              atomicAdd(&acc[s * BS2 + i * GD + jj], K[i][jj]);
+              atomicAdd(&acc[s * BS2 + i * GD + jj], K[bb][i][jj]);
       }
     } else if constexpr (SIMP) {
       // affine simplex: G_ab = |J| Ji^T Ahat_ab Ji  (reference-tensor form)
@@ -1374,6 +1391,9 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s) {
   return FA_OK;
 }
 
+#ifndef FA_NEO_NSPLIT
+#define FA_NEO_NSPLIT 10  // measured (n=120 sweep): 10 > 5 > 2
+#endif
 #ifndef FA_P2TET_NSPLIT
 #define FA_P2TET_NSPLIT 2  // measured best with the reference-tensor blocks (n=120 sweep)
 #endif
@@ -1383,7 +1403,7 @@ static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const
   const int ct = m->cell_type, p = m->degree, nq = T.nq;
   if (kind == FA_ASYM_DAMAGE) return launch_gather<2, 3, 3, 1, 1, FA_ASYM_DAMAGE>(P, bc, s);
   if (kind == FA_NEO_HOOKEAN) {
-    if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, 5, FA_NEO_HOOKEAN>(P, bc, s);
+    if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, FA_NEO_NSPLIT, FA_NEO_HOOKEAN>(P, bc, s);
     if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, FA_NEO_HOOKEAN>(P, bc, s);
     if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, FA_NEO_HOOKEAN>(P, bc, s);
     if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, FA_NEO_HOOKEAN>(P, bc, s);
