@@ -137,6 +137,11 @@ extern "C" int fa_element_info(int32_t cell_type, int32_t degree, int32_t qdeg, 
   return FA_OK;
 }
 
+// AMD dispatches are limited to < 2^32 work-items (a larger grid fails silently): every kernel is
+// grid-stride and grids are capped at kMaxBlocks (x 256 threads < 2^32; multiple of 8 for the
+// XCD-aware gather order).
+static constexpr int64_t kMaxBlocks = (1 << 24) - 8;
+
 // ------------------------------------------------------------------------------------ device math
 // Kernel-side views (passed by value).
 struct MeshView {
@@ -617,6 +622,158 @@ __global__ void k_zero_window(BsrView A, int bs2) {
     A.data[i] = 0.0;
 }
 
+// ------------------------------------------------------------------------------------ hexahedra: MFMA
+// Q1/Q2/Q3 hexahedra, linear elasticity, any trilinear geometry. One 256-thread workgroup per cell.
+// With Phi_i[q][a] = sqrt(w_q |J_q|) d_i phi_a(x_q) (physical gradients), the cell's
+// grad-grad products are nine small GEMMs  M_ik = Phi_i Phi_k^T  (NN x NN, inner dim = quadrature
+// points), a genuine per-cell contraction that runs on v_mfma_f64_16x16x4_f64; the elasticity
+// block is then register-local: K_ab[i][k] = lam M_ik[a][b] + mu M_ki[a][b] + mu d_ik tr M[a][b].
+// Each lane ends with complete 3x3 blocks (4 (a,b) pairs per 16x16 tile), which MODE 0 writes to
+// Ae and MODE 1 adds into the global BSR with FP64 atomics (dolfinx ADD_VALUES semantics).
+typedef double fa_d4 __attribute__((ext_vector_type(4)));
+
+template <int NN, int NQ, int MODE>
+__global__ __launch_bounds__(64 * ((NN + 15) / 16) * ((NN + 15) / 16)) void k_hex_mfma(
+    MeshView M, FormView F, DevTables T, int64_t c0, int64_t ncells, double* __restrict__ Ae, BsrView A,
+    const int8_t* __restrict__ bc, int* __restrict__ err) {
+  constexpr int NT = (NN + 15) / 16;  // 16-row tiles per side; one wave per (a, b) tile
+  constexpr int NTHR = 64 * NT * NT;
+  constexpr int NNP = NT * 16 + 16;   // row stride: +16 doubles puts q and q+1 on opposite bank halves
+  constexpr int QMAX = (NQ + 3) & ~3;
+  __shared__ double phi[3][QMAX][NNP];
+  __shared__ double sJ[QMAX][10];  // Ji (9) + sqrt(w |J|)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nq = NQ, nqp = QMAX;
+  for (int64_t ci = blockIdx.x; ci < ncells; ci += gridDim.x) {
+    const int64_t c = c0 + ci;
+    __syncthreads();
+    if (tid < nq) {  // geometry at quadrature point q = tid
+      double xv[8][3];
+      const int32_t* gv = M.geom + c * 8;
+#pragma unroll
+      for (int v = 0; v < 8; ++v)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) xv[v][i] = M.x[(int64_t)gv[v] * 3 + i];
+      double Ji[3][3];
+      const double det = tensor_geometry<3, 8>(xv, T.gdphi + tid * 24, Ji);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sJ[tid][i * 3 + k] = Ji[i][k];
+      sJ[tid][9] = sqrt(T.wq[tid] * fabs(det));
+    }
+    __syncthreads();
+    for (int idx = tid; idx < nqp * NNP; idx += NTHR) {
+      const int q = idx / NNP, a = idx % NNP;
+      double g[3] = {0.0, 0.0, 0.0};
+      if (q < nq && a < NN) {
+        const double* dp = T.dphi + ((size_t)q * NN + a) * 3;
+        const double sc = sJ[q][9];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) g[d] = sc * (dp[0] * sJ[q][d] + dp[1] * sJ[q][3 + d] + dp[2] * sJ[q][6 + d]);
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) phi[i][q][a] = g[i];
+    }
+    __syncthreads();
+    double lam, mu;
+    cell_lame(F, c, lam, mu);
+    const int32_t* cn = M.cells + c * NN;
+    for (int t = wave; t < NT * NT; t += NT * NT) {
+      const int ta = t / NT, tb = t % NT;
+      fa_d4 acc[9];
+#pragma unroll
+      for (int m = 0; m < 9; ++m) acc[m] = fa_d4{0.0, 0.0, 0.0, 0.0};
+      const int ra = ta * 16 + (lane & 15), rb = tb * 16 + (lane & 15), kq = lane >> 4;
+      for (int q0 = 0; q0 < nqp; q0 += 4) {
+        double av[3], bv[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          av[i] = phi[i][q0 + kq][ra];  // A[a][q] = Phi_i
+          bv[i] = phi[i][q0 + kq][rb];  // B[q][b] = Phi_k^T
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) acc[i * 3 + k] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[k], acc[i * 3 + k], 0, 0, 0);
+      }
+      // D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * r
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int a = ta * 16 + (lane >> 4) + 4 * r, b = tb * 16 + (lane & 15);
+        if (a >= NN || b >= NN) continue;
+        double K[3][3];
+        const double tr = acc[0][r] + acc[4][r] + acc[8][r];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) K[i][k] = lam * acc[i * 3 + k][r] + mu * acc[k * 3 + i][r] + (i == k ? mu * tr : 0.0);
+        if (MODE == 0) {
+          double* out = Ae + ci * (int64_t)(3 * NN) * (3 * NN);
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) out[(a * 3 + i) * (3 * NN) + b * 3 + k] = K[i][k];
+        } else if (MODE == 2) {  // block store for the row gather: Eb[c][a][b][3][3], bc rows/cols zeroed
+          double* out = Ae + ((ci * NN + a) * NN + b) * 9;
+          const int64_t na = cn[a], nb = cn[b];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const bool ri = bc && bc[na * 3 + i];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) out[i * 3 + k] = (ri || (bc && bc[nb * 3 + k])) ? 0.0 : K[i][k];
+          }
+        } else {
+          const int64_t na = cn[a], nb = cn[b];
+          if (na < A.row_begin || na >= A.row_end) continue;
+          const int64_t sl = find_slot(A.indptr, A.indices, na, (int32_t)nb);
+          if (sl < 0) {
+            atomicOr(err, 1);
+            continue;
+          }
+          double* dst = A.data + (sl - A.indptr[A.row_begin]) * 9;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            if (bc && bc[na * 3 + i]) continue;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              if (bc && bc[nb * 3 + k]) continue;
+              unsafeAtomicAdd(dst + i * 3 + k, K[i][k]);
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+static int launch_hex_mfma(int mode, const fa_mesh* mesh, const MeshView& M, const FormView& F, const DevTables& T,
+                           int64_t c0, int64_t nc, double* Ae, const BsrView& A, const int8_t* bc, int* derr,
+                           hipStream_t s, bool* handled) {
+  *handled = false;
+  if (mesh->cell_type != FA_HEXAHEDRON || F.kind != FA_LINEAR_ELASTICITY || nc <= 0) return FA_OK;
+  *handled = true;
+  const int grid = (int)std::min<int64_t>(nc, kMaxBlocks);
+#define HEXL(NN, NQ)                                                                                          \
+  do {                                                                                                        \
+    constexpr int thr = 64 * ((NN + 15) / 16) * ((NN + 15) / 16);                                             \
+    if (mode == 0) k_hex_mfma<NN, NQ, 0><<<grid, thr, 0, s>>>(M, F, T, c0, nc, Ae, A, bc, derr);               \
+    else if (mode == 2) k_hex_mfma<NN, NQ, 2><<<grid, thr, 0, s>>>(M, F, T, c0, nc, Ae, A, bc, derr);          \
+    else k_hex_mfma<NN, NQ, 1><<<grid, thr, 0, s>>>(M, F, T, c0, nc, Ae, A, bc, derr);                        \
+  } while (0)
+  // the default (UFL-estimated) rules: Q1 2^3, Q2 3^3, Q3 4^3 points
+  if (mesh->nn == 8 && T.nq == 8) HEXL(8, 8);
+  else if (mesh->nn == 27 && T.nq == 27) HEXL(27, 27);
+  else if (mesh->nn == 64 && T.nq == 64) HEXL(64, 64);
+  else {
+    *handled = false;
+    return FA_OK;
+  }
+#undef HEXL
+  LAUNCH_CHECK();
+  return FA_OK;
+}
+
 // set bc diagonal entries (after scatter): thread per dof
 template <int GD>
 __global__ void k_bc_diag(BsrView A, int64_t nnodes, const int8_t* __restrict__ bc, double diag, int* err) {
@@ -651,6 +808,10 @@ static constexpr int kGatherLdsValues = FA_GATHER_LDS;  // accumulator bytes per
 static constexpr int kGatherMaxAdj = 512;       // adjacency entries per chunk
 static constexpr int kGatherMaxRows = 128;      // rows per chunk
 
+// gather variant whose blocks come from a per-cell block store [cell][a][b][GD][GD] (hexahedra:
+// written by the MFMA kernel) instead of being computed from a record
+constexpr int MAT_BLOCKS = 9;
+
 template <int GD, int NV, int NQ, int MAT>
 struct Rec {
   static constexpr bool SIMP = (NV == GD + 1);
@@ -658,7 +819,8 @@ struct Rec {
   static constexpr int NTRI = N * (N + 1) / 2;  // stored upper triangle of the tangent
   // LIN simplex: Ji[GD*GD], wdet, lam, mu | LIN tensor: NQ x (Ji[GD*GD], wdet), lam, mu |
   // DAMAGE (P1 tri): g[3][2], w, H[3][3] | NEO (simplex): Ji[GD*GD], wdet, NQ x A_q upper triangle
-  static constexpr int RAW = MAT == FA_ASYM_DAMAGE ? 16
+  static constexpr int RAW = MAT == MAT_BLOCKS ? 2
+                             : MAT == FA_ASYM_DAMAGE ? 16
                              : MAT == FA_NEO_HOOKEAN ? N + 1 + NQ * NTRI
                                                      : (SIMP ? GD * GD + 3 : NQ * (GD * GD + 1) + 2);
   static constexpr int SIZE = (RAW + 1) & ~1;  // even: 16-byte aligned records
@@ -817,8 +979,9 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   __shared__ int32_t rowoff[kGatherMaxRows + 1];
   __shared__ uint8_t adjrow[kGatherMaxAdj];
   constexpr bool NEO = (MAT == FA_NEO_HOOKEAN);
-  __shared__ double s_w[SIMP && !NEO ? 1 : NQ];
-  __shared__ double s_dphi[SIMP && !NEO ? 1 : NQ * NN * GD];
+  constexpr bool TAB = (MAT != MAT_BLOCKS) && (NEO || !SIMP);  // quadrature tables staged in LDS
+  __shared__ double s_w[TAB ? NQ : 1];
+  __shared__ double s_dphi[TAB ? NQ * NN * GD : 1];
   __shared__ double s_ahat[SIMP ? NN * NN * BS2 : 1];
 
   // XCD-aware chunk order: blocks b and b+8 share an XCD (round-robin dispatch), so XCD
@@ -844,7 +1007,8 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     int64_t j0 = P.adj_ptr[r0 + t], j1 = P.adj_ptr[r0 + t + 1];
     for (int64_t j = j0; j < j1; ++j) adjrow[j - a0] = (uint8_t)t;
   }
-  if constexpr (NEO) {
+  if constexpr (MAT == MAT_BLOCKS) {
+  } else if constexpr (NEO) {
     for (int t = tid; t < NQ; t += 256) s_w[t] = P.tab[t];
     for (int t = tid; t < NQ * NN * GD; t += 256) s_dphi[t] = P.tab[NQ + t];
   } else if constexpr (SIMP) {
@@ -866,12 +1030,14 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     // one record + the column nodes + the bc mask: all independent loads, issued together
     constexpr int RL = NEO ? ((BS2 + 2) & ~1) : R::SIZE;  // registers: NEO keeps only Ji, wdet
     double r[RL];
-    const double2* rp = reinterpret_cast<const double2*>(P.rec + c * R::SIZE);
+    if constexpr (MAT != MAT_BLOCKS) {
+      const double2* rp = reinterpret_cast<const double2*>(P.rec + c * R::SIZE);
 #pragma unroll
-    for (int k = 0; k < RL / 2; ++k) {
-      double2 v = rp[k];
-      r[2 * k] = v.x;
-      r[2 * k + 1] = v.y;
+      for (int k = 0; k < RL / 2; ++k) {
+        double2 v = rp[k];
+        r[2 * k] = v.x;
+        r[2 * k + 1] = v.y;
+      }
     }
     int32_t cn[NBG];
 #pragma unroll
@@ -881,7 +1047,18 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     }
     const uint32_t mask = P.bcmask ? P.bcmask[c] : 0u;
 
-    if constexpr (MAT == FA_ASYM_DAMAGE) {
+    if constexpr (MAT == MAT_BLOCKS) {
+      const double* Eb = P.rec + ((int64_t)c * NN + aloc) * NN * BS2;  // bc already applied
+#pragma unroll 1
+      for (int bb = 0; bb < NBG; ++bb) {
+        const int b = part * NBG + bb;
+        if (b >= NN) break;
+        const int s = lds_find(cols, lo, hi, cn[bb]);
+        if (s < 0) { atomicOr(P.err, 1); continue; }
+#pragma unroll
+        for (int e = 0; e < BS2; ++e) atomicAdd(&acc[s * BS2 + e], Eb[b * BS2 + e]);
+      }
+    } else if constexpr (MAT == FA_ASYM_DAMAGE) {
       double H[3][3];
 #pragma unroll
       for (int i = 0; i < 3; ++i)
@@ -1108,7 +1285,6 @@ __global__ void k_row_ptr_from_sorted(const int32_t* __restrict__ keys, int64_t 
 
 // AMD dispatches are limited to < 2^32 work-items in total (a larger grid fails silently),
 // so grids are capped and every kernel is written grid-stride.
-static constexpr int64_t kMaxBlocks = (1 << 24) - 8;  // 2^24 x 256 threads < 2^32; multiple of 8
 static int grid_for(int64_t n, int block = 256) {
   int64_t g = (n + block - 1) / block;
   if (g < 1) g = 1;
@@ -1397,9 +1573,41 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s) {
 #ifndef FA_P2TET_NSPLIT
 #define FA_P2TET_NSPLIT 2  // measured best with the reference-tensor blocks (n=120 sweep)
 #endif
+// Hexahedra: MFMA element blocks into a stream-ordered block store, then the row gather sums
+// them (the "store pass + per-destination sum pass" alternative to global atomics).
+template <int NN, int NQ, int NSPLIT>
+static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc, hipStream_t s) {
+  const int64_t nc = P.M.ncells;
+  double* eb = nullptr;
+  int rc;
+  if ((rc = scratch_alloc((void**)&eb, sizeof(double) * 9 * NN * NN * nc, s))) return rc;
+  if (nc > 0) {
+    constexpr int thr = 64 * ((NN + 15) / 16) * ((NN + 15) / 16);
+    const int grid = (int)std::min<int64_t>(nc, kMaxBlocks);
+    BsrView none{nullptr, nullptr, nullptr, 0, 0};
+    k_hex_mfma<NN, NQ, 2><<<grid, thr, 0, s>>>(P.M, P.F, T, 0, nc, eb, none, bc, P.err);
+    LAUNCH_CHECK();
+  }
+  P.rec = eb;
+  P.bcmask = nullptr;
+  if (P.nchunks > 0) {
+    const int64_t per = (P.nchunks + 7) / 8;
+    const int64_t grid = std::min<int64_t>(8 * per, kMaxBlocks);
+    k_gather<3, NN, 8, NQ, NSPLIT, MAT_BLOCKS><<<(unsigned)grid, 256, 0, s>>>(P);
+    LAUNCH_CHECK();
+  }
+  HIP_TRY(hipFreeAsync(eb, s));
+  return FA_OK;
+}
+
 static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const GatherArgs& P, const int8_t* bc,
                            hipStream_t s, bool* handled) {
   *handled = true;
+  if (m->cell_type == FA_HEXAHEDRON && kind == FA_LINEAR_ELASTICITY) {
+    if (m->degree == 1 && T.nq == 8) return launch_hex_gather<8, 8, 1>(P, T, bc, s);
+    if (m->degree == 2 && T.nq == 27) return launch_hex_gather<27, 27, 3>(P, T, bc, s);
+    if (m->degree == 3 && T.nq == 64) return launch_hex_gather<64, 64, 8>(P, T, bc, s);
+  }
   const int ct = m->cell_type, p = m->degree, nq = T.nq;
   if (kind == FA_ASYM_DAMAGE) return launch_gather<2, 3, 3, 1, 1, FA_ASYM_DAMAGE>(P, bc, s);
   if (kind == FA_NEO_HOOKEAN) {
@@ -1455,6 +1663,9 @@ extern "C" int fa_tabulate_cells(const fa_mesh* mesh, const fa_form* form, int64
   if ((rc = get_tables(mesh->cell_type, mesh->degree, form->qdeg, &T))) return rc;
   MeshView M{mesh->cells, mesh->geom, mesh->x, mesh->ncells, mesh->nnodes, mesh->nn, mesh->nv, mesh->gdim};
   BsrView A{nullptr, nullptr, nullptr, 0, 0};
+  bool hex = false;
+  rc = launch_hex_mfma(0, mesh, M, F, T, c0, ncells_out, Ae, A, nullptr, nullptr, (hipStream_t)stream, &hex);
+  if (rc || hex) return rc;
   return launch_cell_blocks(0, mesh, M, F, T, c0, ncells_out, Ae, A, nullptr, nullptr, (hipStream_t)stream);
 }
 
@@ -1502,7 +1713,10 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
       k_zero_window<<<4096, 256, 0, s>>>(Av, A->bs * A->bs);
       LAUNCH_CHECK();
     }
-    rc = launch_cell_blocks(1, mesh, M, F, T, 0, mesh->ncells, nullptr, Av, bc, derr, s);
+    bool hex = false;
+    rc = launch_hex_mfma(1, mesh, M, F, T, 0, mesh->ncells, nullptr, Av, bc, derr, s, &hex);
+    if (rc) return rc;
+    if (!hex) rc = launch_cell_blocks(1, mesh, M, F, T, 0, mesh->ncells, nullptr, Av, bc, derr, s);
     if (rc) return rc;
     if (bc) {
       int64_t n = (we - wb) * mesh->gdim;
