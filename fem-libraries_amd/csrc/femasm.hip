@@ -964,6 +964,9 @@ __device__ __forceinline__ int lds_find(const int32_t* cols, int lo, int hi, int
 #ifndef FA_GATHER_WAVES
 #define FA_GATHER_WAVES 4  // min waves per SIMD: 4 -> <= 128 VGPRs (16 waves / CU); measured best
 #endif
+#ifndef FA_GATHER_PERMUTE
+#define FA_GATHER_PERMUTE 0
+#endif
 #ifndef FA_GATHER_UNROLL_B
 #define FA_GATHER_UNROLL_B 1
 #endif
@@ -1020,7 +1023,18 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   __syncthreads();
 
   const int nitems = na * NSPLIT;
-  for (int it = tid; it < nitems; it += 256) {
+#if FA_GATHER_PERMUTE
+  // consecutive items belong to the same row and add into the same LDS slots (the diagonal
+  // block of a vertex row gets ~24 adds); a stride coprime to nitems spreads rows over lanes
+  int stride = 97;
+  while (nitems % stride == 0 && stride > 1) stride -= 2;
+#endif
+  for (int it0 = tid; it0 < nitems; it0 += 256) {
+#if FA_GATHER_PERMUTE
+    const int it = (int)(((int64_t)it0 * stride) % nitems);
+#else
+    const int it = it0;
+#endif
     const int j = it / NSPLIT, part = it % NSPLIT;
     const int32_t pflat = P.adj_idx[a0 + j];
     const int64_t c = pflat / NN;
