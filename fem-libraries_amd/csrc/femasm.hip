@@ -965,7 +965,7 @@ __device__ __forceinline__ int lds_find(const int32_t* cols, int lo, int hi, int
 #define FA_GATHER_WAVES 4  // min waves per SIMD: 4 -> <= 128 VGPRs (16 waves / CU); measured best
 #endif
 #ifndef FA_GATHER_PERMUTE
-#define FA_GATHER_PERMUTE 0
+#define FA_GATHER_PERMUTE 1  // measured +4 % on config E (fewer same-slot LDS adds per instruction)
 #endif
 #ifndef FA_GATHER_UNROLL_B
 #define FA_GATHER_UNROLL_B 1
@@ -1042,7 +1042,8 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     const int lr = adjrow[j];
     const int lo = rowoff[lr], hi = rowoff[lr + 1];
     // one record + the column nodes + the bc mask: all independent loads, issued together
-    constexpr int RL = NEO ? ((BS2 + 2) & ~1) : R::SIZE;  // registers: NEO keeps only Ji, wdet
+    // registers: NEO keeps only Ji, wdet; tensor cells read their per-q records in the q loop
+    constexpr int RL = NEO ? ((BS2 + 2) & ~1) : (SIMP || MAT == FA_ASYM_DAMAGE ? R::SIZE : 2);
     double r[RL];
     if constexpr (MAT != MAT_BLOCKS) {
       const double2* rp = reinterpret_cast<const double2*>(P.rec + c * R::SIZE);
@@ -1212,49 +1213,57 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
               atomicAdd(&acc[s * BS2 + i * GD + jj], K[i][jj]);
       }
     } else {
-      const double lam = r[NQ * (BS2 + 1)];
-      const double mu = r[NQ * (BS2 + 1) + 1];
-      // weighted physical gradients of the row node at every quadrature point
-      double ga[NQ][GD];
+      // non-affine tensor cells: J^-1 per quadrature point, read from the record as the rolled
+      // q loop needs it; only the per-column accumulators G stay live
+      const double* rq = P.rec + c * R::SIZE;
+      const double lam = rq[NQ * (BS2 + 1)];
+      const double mu = rq[NQ * (BS2 + 1) + 1];
+      double G[NBG][GD][GD];
 #pragma unroll
+      for (int bb = 0; bb < NBG; ++bb)
+#pragma unroll
+        for (int i = 0; i < GD; ++i)
+#pragma unroll
+          for (int k = 0; k < GD; ++k) G[bb][i][k] = 0.0;
+#pragma unroll 1
       for (int q = 0; q < NQ; ++q) {
-        const double* Jq = r + q * (BS2 + 1);
-        const double wd = s_w[q] * Jq[BS2];
+        const double* Jq = rq + q * (BS2 + 1);
+        double Jl[BS2 + 1];
+#pragma unroll
+        for (int e = 0; e <= BS2; ++e) Jl[e] = Jq[e];
+        const double wd = s_w[q] * Jl[BS2];
+        double ga[GD];
 #pragma unroll
         for (int d = 0; d < GD; ++d) {
           double sgd = 0.0;
 #pragma unroll
-          for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + aloc) * GD + k] * Jq[k * GD + d];
-          ga[q][d] = wd * sgd;
+          for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + aloc) * GD + k] * Jl[k * GD + d];
+          ga[d] = wd * sgd;
         }
-      }
-#pragma unroll FA_GATHER_UNROLL_B
-      for (int bb = 0; bb < NBG; ++bb) {
-        const int b = part * NBG + bb;
-        if (b >= NN) break;
-        double G[GD][GD];
 #pragma unroll
-        for (int i = 0; i < GD; ++i)
-#pragma unroll
-          for (int k = 0; k < GD; ++k) G[i][k] = 0.0;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const double* Jq = r + q * (BS2 + 1);
+        for (int bb = 0; bb < NBG; ++bb) {
+          const int b = part * NBG + bb;
+          if (b >= NN) break;
           double gb[GD];
 #pragma unroll
           for (int d = 0; d < GD; ++d) {
             double sgd = 0.0;
 #pragma unroll
-            for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + b) * GD + k] * Jq[k * GD + d];
+            for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + b) * GD + k] * Jl[k * GD + d];
             gb[d] = sgd;
           }
 #pragma unroll
           for (int i = 0; i < GD; ++i)
 #pragma unroll
-            for (int k = 0; k < GD; ++k) G[i][k] += ga[q][i] * gb[k];
+            for (int k = 0; k < GD; ++k) G[bb][i][k] += ga[i] * gb[k];
         }
+      }
+#pragma unroll
+      for (int bb = 0; bb < NBG; ++bb) {
+        const int b = part * NBG + bb;
+        if (b >= NN) break;
         double K[GD][GD];
-        lin_block<GD>(G, lam, mu, K);
+        lin_block<GD>(G[bb], lam, mu, K);
         const int s = lds_find(cols, lo, hi, cn[bb]);
         if (s < 0) { atomicOr(P.err, 1); continue; }
 #pragma unroll
