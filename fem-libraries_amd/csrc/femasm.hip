@@ -468,6 +468,19 @@ __device__ void neo_tangent_ad(const double (&F)[GD * GD], double lam, double mu
     }
 }
 
+// P[iJ] = d psi / dF_iJ (first Piola stress) by forward-mode AD: the residual of the same potential.
+template <int GD>
+__device__ void neo_stress_ad(const double (&F)[GD * GD], double lam, double mu, double (&P)[GD * GD]) {
+  constexpr int N = GD * GD;
+  using D1 = Dual<double>;
+  for (int i = 0; i < N; ++i) {
+    D1 x[N];
+#pragma unroll
+    for (int m = 0; m < N; ++m) x[m] = D1{F[m], m == i ? 1.0 : 0.0};
+    P[i] = neo_psi<GD, D1>(x, lam, mu).d;
+  }
+}
+
 // F at a quadrature point from the cell's nodal displacements and physical gradients.
 template <int GD>
 __device__ __forceinline__ void deformation_gradient(const double* __restrict__ u, const int32_t* cn, int nn,
@@ -838,6 +851,7 @@ struct GatherArgs {
   const int32_t* adj_idx;
   const int64_t* row_start;
   int64_t nchunks;
+  const uint16_t* slots;  // optional [adjacency entry][NN] position of the block within its row
   const int8_t* bc;
   double diag;
   const double* tab;  // device tables: wq | dphi | gdphi
@@ -1068,7 +1082,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       for (int bb = 0; bb < NBG; ++bb) {
         const int b = part * NBG + bb;
         if (b >= NN) break;
-        const int s = lds_find(cols, lo, hi, cn[bb]);
+        const int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_find(cols, lo, hi, cn[bb]);
         if (s < 0) { atomicOr(P.err, 1); continue; }
 #pragma unroll
         for (int e = 0; e < BS2; ++e) atomicAdd(&acc[s * BS2 + e], Eb[b * BS2 + e]);
@@ -1088,7 +1102,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
         double gb[2] = {r[2 * b], r[2 * b + 1]};
         double K[2][2];
         damage_block(ga, gb, w, H, K);
-        const int s = lds_find(cols, lo, hi, cn[bb]);
+        const int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_find(cols, lo, hi, cn[bb]);
         if (s < 0) { atomicOr(P.err, 1); continue; }
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -1164,7 +1178,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       for (int bb = 0; bb < NBG; ++bb) {
         const int b = part * NBG + bb;
         if (b >= NN) break;
-        const int s = lds_find(cols, lo, hi, cn[bb]);
+        const int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_find(cols, lo, hi, cn[bb]);
         if (s < 0) { atomicOr(P.err, 1); continue; }
 #pragma unroll
         for (int i = 0; i < GD; ++i)
@@ -1203,7 +1217,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
           }
         double K[GD][GD];
         lin_block<GD>(G, lam, mu, K);
-        const int s = lds_find(cols, lo, hi, cn[bb]);
+        const int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_find(cols, lo, hi, cn[bb]);
         if (s < 0) { atomicOr(P.err, 1); continue; }
 #pragma unroll
         for (int i = 0; i < GD; ++i)
@@ -1264,7 +1278,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
         if (b >= NN) break;
         double K[GD][GD];
         lin_block<GD>(G[bb], lam, mu, K);
-        const int s = lds_find(cols, lo, hi, cn[bb]);
+        const int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_find(cols, lo, hi, cn[bb]);
         if (s < 0) { atomicOr(P.err, 1); continue; }
 #pragma unroll
         for (int i = 0; i < GD; ++i)
@@ -1476,6 +1490,59 @@ extern "C" int fa_sparsity_fill(const fa_mesh* mesh, const fa_adjacency* adj, co
 }
 
 // ------------------------------------------------------------------------------------ gather plan
+// slot map: thread per row node; for each adjacency entry of the row and each column node of the
+// cell, the position of that column in the row (binary search once, at plan time)
+__global__ void k_build_slots(MeshView M, const int64_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj_idx,
+                              const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+                              uint16_t* __restrict__ slots, int* err) {
+  const int nn = M.nn;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < M.nnodes; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b0 = indptr[r], b1 = indptr[r + 1];
+    if (b1 - b0 > 65535) {
+      atomicOr(err, 8);
+      continue;
+    }
+    for (int64_t j = adj_ptr[r]; j < adj_ptr[r + 1]; ++j) {
+      const int64_t c = adj_idx[j] / nn;
+      for (int b = 0; b < nn; ++b) {
+        const int32_t col = M.cells[c * nn + b];
+        int64_t lo = b0, hi = b1 - 1, s = -1;
+        while (lo <= hi) {
+          int64_t mid = (lo + hi) >> 1;
+          if (indices[mid] == col) { s = mid; break; }
+          if (indices[mid] < col) lo = mid + 1; else hi = mid - 1;
+        }
+        if (s < 0) { atomicOr(err, 1); s = b0; }
+        slots[j * nn + b] = (uint16_t)(s - b0);
+      }
+    }
+  }
+}
+
+extern "C" int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, uint16_t* slots,
+                             fa_plan* plan, void* stream) {
+  int rc = check_mesh(mesh);
+  if (rc) return rc;
+  if (!adj || !A || !slots || !plan) return fail(FA_E_ARG, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  MeshView M{mesh->cells, mesh->geom, mesh->x, mesh->ncells, mesh->nnodes, mesh->nn, mesh->nv, mesh->gdim};
+  int* derr = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&derr, sizeof(int), s));
+  HIP_TRY(hipMemsetAsync(derr, 0, sizeof(int), s));
+  if (mesh->nnodes > 0) {
+    k_build_slots<<<grid_for(mesh->nnodes), 256, 0, s>>>(M, adj->ptr, adj->idx, A->indptr, A->indices, slots, derr);
+    LAUNCH_CHECK();
+  }
+  int herr = 0;
+  HIP_TRY(hipMemcpyAsync(&herr, derr, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipFreeAsync(derr, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (herr & 8) return fail(FA_E_CAPACITY, "a row holds more than 65535 blocks");
+  if (herr) return fail(FA_E_PATTERN, "sparsity pattern misses a (row, column) pair of a cell");
+  plan->slots = slots;
+  return FA_OK;
+}
+
 extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int64_t* row_start,
                               fa_plan* plan, void* stream) {
   int rc = check_mesh(mesh);
@@ -1521,6 +1588,7 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
   plan->row_start = row_start;
   plan->max_blocks = mb;
   plan->max_adj = ma;
+  plan->slots = nullptr;
   return FA_OK;
 }
 
@@ -1722,6 +1790,7 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     GatherArgs P;
     P.M = M; P.F = F; P.A = Av;
     P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks;
+    P.slots = plan->slots;
     P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr;
     bool handled = false;
     rc = dispatch_gather(mesh, T, F.kind, P, bc, s, &handled);
@@ -1862,6 +1931,22 @@ __global__ __launch_bounds__(256) void k_vector(MeshView M, FormView F, DevTable
                 for (int k = 0; k < GD; ++k) gu[i][k] += ui * gb[k];
               }
             }
+            if (F.kind == FA_NEO_HOOKEAN) {  // r_a,i += w P_iK(I + grad u) g_a[K]
+              double Fq[GD * GD], P[GD * GD];
+#pragma unroll
+              for (int i = 0; i < GD; ++i)
+#pragma unroll
+                for (int k = 0; k < GD; ++k) Fq[i * GD + k] = gu[i][k] + (i == k ? 1.0 : 0.0);
+              neo_stress_ad<GD>(Fq, lam, mu, P);
+#pragma unroll
+              for (int i = 0; i < GD; ++i) {
+                double s = 0.0;
+#pragma unroll
+                for (int k = 0; k < GD; ++k) s += P[i * GD + k] * ga[k];
+                r[i] += wd * s;
+              }
+              continue;
+            }
             double tr = 0.0;
 #pragma unroll
             for (int i = 0; i < GD; ++i) tr += gu[i][i];
@@ -1937,6 +2022,24 @@ __global__ __launch_bounds__(256) void k_lifting(MeshView M, FormView F, DevTabl
             damage_cell(M, F, c, gg, w, H);
             double ga[2] = {gg[aloc][0], gg[aloc][1]}, gb[2] = {gg[bb][0], gg[bb][1]};
             damage_block(ga, gb, w, H, K);
+          }
+        } else if (F.kind == FA_NEO_HOOKEAN) {  // K_ab of the tangent at the state u
+          double lam, mu;
+          cell_lame(F, c, lam, mu);
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int k = 0; k < GD; ++k) K[i][k] = 0.0;
+          for (int q = 0; q < T.nq; ++q) {
+            double Ji[GD][GD];
+            const double wd = T.wq[q] * cell_geometry_q<GD, NV>(M, c, T.gdphi + (size_t)q * NV * GD, Ji);
+            double Fq[GD * GD], A[GD * GD * GD * GD];
+            deformation_gradient<GD>(F.u, cn, nn, T.dphi + (size_t)q * nn * GD, Ji, Fq);
+            neo_tangent_ad<GD>(Fq, lam, mu, A);
+            double ga[GD], gb[GD];
+            phys_grad<GD>(T.dphi + ((size_t)q * nn + aloc) * GD, Ji, ga);
+            phys_grad<GD>(T.dphi + ((size_t)q * nn + bb) * GD, Ji, gb);
+            neo_block_add<GD>(A, ga, gb, wd, K);
           }
         } else {
           double lam, mu;
@@ -2031,6 +2134,77 @@ extern "C" int fa_set_bc(double* b, int64_t ndofs, const int8_t* bc, const doubl
   if (!b || !bc || !g) return fail(FA_E_ARG, "null argument");
   if (ndofs <= 0) return FA_OK;
   k_set_bc<<<grid_for(ndofs), 256, 0, (hipStream_t)stream>>>(b, ndofs, bc, g, x0, alpha);
+  LAUNCH_CHECK();
+  return FA_OK;
+}
+
+// ------------------------------------------------------------------------------------ BSR SpMV
+// y = A x over the row window (the Newton driver's Krylov solver): one thread
+// per block row, blocks streamed in order.
+template <int BS>
+__global__ __launch_bounds__(256) void k_bsr_mult(BsrView A, const double* __restrict__ x, double* __restrict__ y) {
+  const int64_t base = A.indptr[A.row_begin];
+  for (int64_t r = A.row_begin + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < A.row_end;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    double acc[BS];
+#pragma unroll
+    for (int i = 0; i < BS; ++i) acc[i] = 0.0;
+    for (int64_t k = A.indptr[r]; k < A.indptr[r + 1]; ++k) {
+      const double* blk = A.data + (k - base) * BS * BS;
+      const int64_t cidx = A.indices[k];
+      double xv[BS];
+#pragma unroll
+      for (int j = 0; j < BS; ++j) xv[j] = x[cidx * BS + j];
+#pragma unroll
+      for (int i = 0; i < BS; ++i)
+#pragma unroll
+        for (int j = 0; j < BS; ++j) acc[i] += blk[i * BS + j] * xv[j];
+    }
+#pragma unroll
+    for (int i = 0; i < BS; ++i) y[r * BS + i] = acc[i];
+  }
+}
+
+extern "C" int fa_bsr_mult(const fa_bsr* A, const double* x, double* y, void* stream) {
+  if (!A || !A->indptr || !A->indices || !A->data || !x || !y) return fail(FA_E_ARG, "null argument");
+  int64_t wb = A->row_begin, we = A->row_end;
+  if (we <= wb) { wb = 0; we = A->nrows; }
+  BsrView Av{A->indptr, A->indices, A->data, wb, we};
+  hipStream_t s = (hipStream_t)stream;
+  const int g = grid_for(we - wb);
+  if (we <= wb) return FA_OK;
+  if (A->bs == 2) k_bsr_mult<2><<<g, 256, 0, s>>>(Av, x, y);
+  else if (A->bs == 3) k_bsr_mult<3><<<g, 256, 0, s>>>(Av, x, y);
+  else if (A->bs == 1) k_bsr_mult<1><<<g, 256, 0, s>>>(Av, x, y);
+  else return fail(FA_E_UNSUPPORTED, "block size %d", A->bs);
+  LAUNCH_CHECK();
+  return FA_OK;
+}
+
+// Diagonal blocks of the row window (block-Jacobi preconditioner of the Newton driver's CG).
+__global__ __launch_bounds__(256) void k_bsr_block_diag(BsrView A, int bs, double* __restrict__ out) {
+  const int64_t base = A.indptr[A.row_begin];
+  for (int64_t r = A.row_begin + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < A.row_end;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    double* o = out + (r - A.row_begin) * bs * bs;
+    for (int i = 0; i < bs * bs; ++i) o[i] = 0.0;
+    int64_t lo = A.indptr[r], hi = A.indptr[r + 1];
+    while (lo < hi) {  // columns are sorted
+      const int64_t mid = (lo + hi) >> 1;
+      if (A.indices[mid] < r) lo = mid + 1; else hi = mid;
+    }
+    if (lo < A.indptr[r + 1] && A.indices[lo] == r)
+      for (int i = 0; i < bs * bs; ++i) o[i] = A.data[(lo - base) * bs * bs + i];
+  }
+}
+
+extern "C" int fa_bsr_block_diag(const fa_bsr* A, double* out, void* stream) {
+  if (!A || !A->indptr || !A->indices || !A->data || !out) return fail(FA_E_ARG, "null argument");
+  int64_t wb = A->row_begin, we = A->row_end;
+  if (we <= wb) { wb = 0; we = A->nrows; }
+  if (we <= wb) return FA_OK;
+  BsrView Av{A->indptr, A->indices, A->data, wb, we};
+  k_bsr_block_diag<<<grid_for(we - wb), 256, 0, (hipStream_t)stream>>>(Av, A->bs, out);
   LAUNCH_CHECK();
   return FA_OK;
 }

@@ -77,6 +77,7 @@ class fa_plan(ctypes.Structure):
         ("row_start", ctypes.c_void_p),
         ("max_blocks", ctypes.c_int32),
         ("max_adj", ctypes.c_int32),
+        ("slots", ctypes.c_void_p),
     ]
 
 
@@ -91,11 +92,14 @@ SIGNATURES = {
     "fa_sparsity_count": (ctypes.c_int, [P, P, P, P, P]),
     "fa_sparsity_fill": (ctypes.c_int, [P, P, P, P, P]),
     "fa_plan_gather": (ctypes.c_int, [P, P, P, P, P, P]),
+    "fa_plan_slots": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_tabulate_cells": (ctypes.c_int, [P, P, I64, I64, P, P]),
     "fa_assemble_matrix": (ctypes.c_int, [P, P, P, P, P, D, P, I32, P]),
     "fa_assemble_vector": (ctypes.c_int, [P, P, P, P, P]),
     "fa_apply_lifting": (ctypes.c_int, [P, P, P, P, P, P, P, D, P]),
     "fa_set_bc": (ctypes.c_int, [P, I64, P, P, P, D, P]),
+    "fa_bsr_mult": (ctypes.c_int, [P, P, P, P]),
+    "fa_bsr_block_diag": (ctypes.c_int, [P, P, P]),
 }
 
 _lib = None

@@ -12,6 +12,7 @@ CPU fallback.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -466,17 +467,7 @@ def create_matrix(a, max_part_bytes: int | None = None) -> MatrixCSR:
 
 
 def _fa_bsr(A: MatrixCSR, part: int = 0) -> _lib.fa_bsr:
-    r0, r1, data = A.parts[part]
-    b = _lib.fa_bsr()
-    b.nrows = A.num_block_rows
-    b.bs = A.bs
-    b.nblocks = A.num_blocks
-    b.indptr = A.indptr.data_ptr()
-    b.indices = A.indices.data_ptr()
-    b.data = data.data_ptr()
-    b.row_begin = r0
-    b.row_end = r1
-    return b
+    return A._fa_bsr(part)
 
 
 def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0):
@@ -490,9 +481,19 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0):
         fb = _fa_bsr(A, part)
         rs = torch.empty(A.parts[part][1] - A.parts[part][0] + 1, dtype=torch.int64, device=V.mesh.device)
         plan = _lib.fa_plan()
+        sh = _lib.stream_handle(V.mesh.device)
         _lib.check(L.fa_plan_gather(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), rs.data_ptr(),
-                                    ctypes.byref(plan), _lib.stream_handle(V.mesh.device)), "fa_plan_gather")
-        plans[key] = (plan, rs, A.indptr)
+                                    ctypes.byref(plan), sh), "fa_plan_gather")
+        slots = None
+        mode = os.environ.get("FEMASM_SLOTS", "auto")
+        # Per (adjacency entry, column node) block position in its row: no LDS search in the
+        # kernel, for 2 B x nn^2 extra reads per cell. Measured (profiles/r1/slots.md): +21% on
+        # Q2 quads (long rows), +2% Q2 hex, -4% P2 tets (config E) -> default: tensor cells only.
+        if mode == "1" or (mode == "auto" and not is_simplex(V.mesh.cell_type)):
+            slots = torch.empty(V.mesh.num_cells * V.nn * V.nn, dtype=torch.int16, device=V.mesh.device)
+            _lib.check(L.fa_plan_slots(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), slots.data_ptr(),
+                                       ctypes.byref(plan), sh), "fa_plan_slots")
+        plans[key] = (plan, rs, A.indptr, slots)
     return plans[key][0]
 
 

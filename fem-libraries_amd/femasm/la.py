@@ -115,13 +115,48 @@ class MatrixCSR:
         out[rows[hit]] = torch.nonzero(hit).reshape(-1)
         return out
 
-    def mult(self, x: torch.Tensor) -> torch.Tensor:
-        """y = A x for a dof vector x [nrows*bs] (torch ops; used by the Newton driver)."""
-        bs = self.bs
-        xb = x.reshape(-1, bs)
-        rows = torch.repeat_interleave(torch.arange(self.num_block_rows, device=x.device),
-                                       self.indptr[1:] - self.indptr[:-1])
-        contrib = torch.bmm(self.data, xb[self.indices.to(torch.int64)].unsqueeze(-1)).squeeze(-1)
-        y = torch.zeros_like(xb)
-        y.index_add_(0, rows, contrib)
-        return y.reshape(-1)
+    def _fa_bsr(self, part: int = 0):
+        """The C-ABI view (fa_bsr) of one row part."""
+        from . import _lib
+
+        r0, r1, data = self.parts[part]
+        b = _lib.fa_bsr()
+        b.nrows = self.num_block_rows
+        b.bs = self.bs
+        b.nblocks = self.num_blocks
+        b.indptr = self.indptr.data_ptr()
+        b.indices = self.indices.data_ptr()
+        b.data = data.data_ptr()
+        b.row_begin = r0
+        b.row_end = r1
+        return b
+
+    def mult(self, x: torch.Tensor, y: torch.Tensor | None = None) -> torch.Tensor:
+        """y = A x for a dof vector x [nrows*bs] (HIP BSR SpMV, fa_bsr_mult, per row part)."""
+        import ctypes
+
+        from . import _lib
+
+        L = _lib.load()
+        if y is None:
+            y = torch.empty_like(x)
+        sh = _lib.stream_handle(x.device)
+        for part in range(len(self.parts)):
+            fb = self._fa_bsr(part)
+            _lib.check(L.fa_bsr_mult(ctypes.byref(fb), x.data_ptr(), y.data_ptr(), sh), "fa_bsr_mult")
+        return y
+
+    def block_diagonal(self) -> torch.Tensor:
+        """Diagonal blocks [nrows, bs, bs] (fa_bsr_block_diag; zeros where a row has none)."""
+        import ctypes
+
+        from . import _lib
+
+        L = _lib.load()
+        out = torch.empty((self.num_block_rows, self.bs, self.bs), dtype=torch.float64, device=self.indices.device)
+        sh = _lib.stream_handle(out.device)
+        for part in range(len(self.parts)):
+            fb = self._fa_bsr(part)
+            r0 = self.parts[part][0]
+            _lib.check(L.fa_bsr_block_diag(ctypes.byref(fb), out[r0:].data_ptr(), sh), "fa_bsr_block_diag")
+        return out

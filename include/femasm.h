@@ -112,6 +112,8 @@ typedef struct {
   const int64_t* row_start;  /* device [nchunks+1] */
   int32_t max_blocks;        /* largest block count of a chunk */
   int32_t max_adj;           /* largest adjacency count of a chunk */
+  const uint16_t* slots;     /* optional device [ncells*nn][nn]: for adjacency entry j and column
+                                node b, the block's position within row j's column list */
 } fa_plan;
 
 const char* fa_last_error(void);
@@ -133,6 +135,12 @@ int fa_sparsity_fill(const fa_mesh* mesh, const fa_adjacency* adj, const int64_t
  * in *plan (synchronises `stream`). */
 int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int64_t* row_start, fa_plan* plan,
                    void* stream);
+
+/* Optional slot map for the gather plan (removes the per-block column search): slots is a
+ * caller-owned device buffer of ncells*nn*nn uint16; on success plan->slots points to it.
+ * Fails with FA_E_CAPACITY if a row holds more than 65535 blocks. */
+int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, uint16_t* slots, fa_plan* plan,
+                  void* stream);
 
 /* Per-cell element matrices Ae [ncells_out][nn*bs][nn*bs] (dof = node*bs + comp) for cells
  * [c0, c0+ncells_out) — the batched ufcx tabulate_tensor / AssembleElementGrad. */
@@ -162,6 +170,15 @@ int fa_apply_lifting(const fa_mesh* mesh, const fa_form* form, const fa_adjacenc
 /* b[i] = alpha * (g[i] - x0[i]) on bc dofs (x0 may be NULL). ndofs = nnodes*bs. */
 int fa_set_bc(double* b, int64_t ndofs, const int8_t* bc, const double* g, const double* x0, double alpha,
               void* stream);
+
+/* y = A x (block rows of A's window; x, y blocked dof vectors). The Krylov kernel of the Newton
+ * driver that consumes the assembled matrix (the reference solves with CG + BoomerAMG,
+ * FEniCSx/mechanic2d/asym_elasto_damage_model.cc:717-813). */
+int fa_bsr_mult(const fa_bsr* A, const double* x, double* y, void* stream);
+
+/* out[r - row_begin] = the diagonal block of block row r (zeros when absent), [rows, bs, bs]:
+ * the block-Jacobi preconditioner of the driver's CG (the reference uses BoomerAMG, :717-813). */
+int fa_bsr_block_diag(const fa_bsr* A, double* out, void* stream);
 
 #ifdef __cplusplus
 }

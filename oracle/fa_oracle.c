@@ -764,9 +764,13 @@ int ora_cell_matrices_elasticity(const ora_mesh* M, const double* lam, const dou
 }
 
 /* ---------------------------------------------------------------- residual & lifting */
+static void neo_stress(int gd, const double* F, double lam, double mu, double* P);
+static void neo_cell(int gd, int nn, int nq, const double* wq, const double* dphi, int nv, const double* gdphi,
+                     const double* xv, const double* uc, double lam, double mu, double* Ae);
 /* dolfinx assemble_vector of F = inner(sigma(u), eps(v)) dx_qs - inner(f, v) dx_qf restated
  * per cell with Voigt vectors: b_e = sum_q w|J| B^T sigma_v - sum_q w|J| N^T f(q); b[dofs] += b_e.
- * kind 0: linear sigma = D B u;  kind 1: reference damage law (P1 tri, centroid, asym_stress).
+ * kind 0: linear sigma = D B u;  kind 1: reference damage law (P1 tri, centroid, asym_stress);
+ * kind 2: neo-Hookean, b_e[a,i] = sum_q w|J| P_iJ(F_q) g_a[J] with F_q = I + grad u.
  * u, f per dof (may be NULL); dnode per node (kind 1). qs < 0: estimated degree. */
 int ora_assemble_residual(const ora_mesh* M, int kind, const double* lam, const double* mu, const double* u,
                           const double* dnode, const double* f, int qs, double* b) {
@@ -810,6 +814,18 @@ int ora_assemble_residual(const ora_mesh* M, int kind, const double* lam, const 
           sv[0] = sig[0]; sv[1] = sig[1]; sv[2] = sig[2];
           for (int i = 0; i < nd; ++i)
             for (int k = 0; k < nvo; ++k) be[i] += B[k * nd + i] * sv[k];
+        } else if (kind == 2) {
+          double F[9], P[9];
+          for (int i = 0; i < gd; ++i)
+            for (int k = 0; k < gd; ++k) {
+              double s = (i == k) ? 1.0 : 0.0;
+              for (int a = 0; a < nn; ++a) s += u[(int64_t)nodes[a] * gd + i] * g[a * gd + k];
+              F[i * gd + k] = s;
+            }
+          neo_stress(gd, F, lam[c], mu[c], P);
+          for (int a = 0; a < nn; ++a)
+            for (int i = 0; i < gd; ++i)
+              for (int k = 0; k < gd; ++k) be[a * gd + i] += w * P[i * gd + k] * g[a * gd + k];
         } else {
           hooke_D(gd, lam[c], mu[c], D);
           for (int k = 0; k < nvo; ++k)
@@ -871,6 +887,10 @@ int ora_apply_lifting(const ora_mesh* M, int kind, const double* lam, const doub
         dq += (dnode ? dnode[nodes[a]] : 0.0) / 3.0;
       }
       ora_damage_cell(xv, uc, dq, lam[c], mu[c], Ae);
+    } else if (kind == 2) {
+      double uc[ORA_MAXN * 3];
+      for (int i = 0; i < nd; ++i) uc[i] = u[(int64_t)nodes[i / gd] * gd + i % gd];
+      neo_cell(gd, nn, nq, wq, dphi, nv, gdphi, xv, uc, lam[c], mu[c], Ae);
     } else {
       ora_elasticity_cell(gd, nn, nq, wq, dphi, nv, gdphi, xv, lam[c], mu[c], Ae);
     }
@@ -888,29 +908,37 @@ int ora_apply_lifting(const ora_mesh* M, int kind, const double* lam, const doub
 /* psi(F) = mu/2 (I_C - 3) - mu ln J + lam/2 (ln J)^2 (2-D: plane strain). Closed-form tangent
  * (independent of the device's AD): with G = F^{-1},
  * A[(iJ)(kL)] = mu d_ik d_JL + (mu - lam ln J) G_Jk G_Li + lam G_Ji G_Lk. */
-static void neo_tangent(int gd, const double* F, double lam, double mu, double* A) {
-  double G[9], J;
+static double neo_inverse(int gd, const double* F, double* G) {
+  double J;
   if (gd == 2) {
     J = F[0] * F[3] - F[1] * F[2];
     G[0] = F[3] / J; G[1] = -F[1] / J; G[2] = -F[2] / J; G[3] = F[0] / J;
   } else {
-    double Jm[9];
-    for (int k = 0; k < 9; ++k) Jm[k] = F[k];
-    double Ji[9];
-    /* reuse the geometry inverse: jacobian() builds J from vertices, so invert directly */
-    J = Jm[0] * (Jm[4] * Jm[8] - Jm[5] * Jm[7]) - Jm[1] * (Jm[3] * Jm[8] - Jm[5] * Jm[6]) +
-        Jm[2] * (Jm[3] * Jm[7] - Jm[4] * Jm[6]);
-    Ji[0] = (Jm[4] * Jm[8] - Jm[5] * Jm[7]) / J;
-    Ji[1] = (Jm[2] * Jm[7] - Jm[1] * Jm[8]) / J;
-    Ji[2] = (Jm[1] * Jm[5] - Jm[2] * Jm[4]) / J;
-    Ji[3] = (Jm[5] * Jm[6] - Jm[3] * Jm[8]) / J;
-    Ji[4] = (Jm[0] * Jm[8] - Jm[2] * Jm[6]) / J;
-    Ji[5] = (Jm[2] * Jm[3] - Jm[0] * Jm[5]) / J;
-    Ji[6] = (Jm[3] * Jm[7] - Jm[4] * Jm[6]) / J;
-    Ji[7] = (Jm[1] * Jm[6] - Jm[0] * Jm[7]) / J;
-    Ji[8] = (Jm[0] * Jm[4] - Jm[1] * Jm[3]) / J;
-    for (int k = 0; k < 9; ++k) G[k] = Ji[k];
+    J = F[0] * (F[4] * F[8] - F[5] * F[7]) - F[1] * (F[3] * F[8] - F[5] * F[6]) + F[2] * (F[3] * F[7] - F[4] * F[6]);
+    G[0] = (F[4] * F[8] - F[5] * F[7]) / J;
+    G[1] = (F[2] * F[7] - F[1] * F[8]) / J;
+    G[2] = (F[1] * F[5] - F[2] * F[4]) / J;
+    G[3] = (F[5] * F[6] - F[3] * F[8]) / J;
+    G[4] = (F[0] * F[8] - F[2] * F[6]) / J;
+    G[5] = (F[2] * F[3] - F[0] * F[5]) / J;
+    G[6] = (F[3] * F[7] - F[4] * F[6]) / J;
+    G[7] = (F[1] * F[6] - F[0] * F[7]) / J;
+    G[8] = (F[0] * F[4] - F[1] * F[3]) / J;
   }
+  return J;
+}
+
+/* First Piola stress P = d psi / dF = mu (F - F^{-T}) + lam ln J F^{-T}. */
+static void neo_stress(int gd, const double* F, double lam, double mu, double* P) {
+  double G[9];
+  double lnJ = log(neo_inverse(gd, F, G));
+  for (int i = 0; i < gd; ++i)
+    for (int Jx = 0; Jx < gd; ++Jx) P[i * gd + Jx] = mu * F[i * gd + Jx] + (lam * lnJ - mu) * G[Jx * gd + i];
+}
+
+static void neo_tangent(int gd, const double* F, double lam, double mu, double* A) {
+  double G[9];
+  double J = neo_inverse(gd, F, G);
   double lnJ = log(J);
   int N = gd * gd;
   for (int i = 0; i < gd; ++i)
@@ -1006,3 +1034,4 @@ int ora_assemble_neohookean(const ora_mesh* M, const double* lam, const double* 
 
 /* public wrapper for tests */
 void ora_neo_tangent(int gd, const double* F, double lam, double mu, double* A) { neo_tangent(gd, F, lam, mu, A); }
+void ora_neo_stress(int gd, const double* F, double lam, double mu, double* P) { neo_stress(gd, F, lam, mu, P); }

@@ -65,6 +65,7 @@ def lib():
         L.ora_assemble_neohookean.argtypes = [ctypes.POINTER(_Mesh), P, P, P, ctypes.c_int, P, ctypes.c_double, P,
                                               P, P, P]
         L.ora_neo_tangent.argtypes = [ctypes.c_int, P, ctypes.c_double, ctypes.c_double, P]
+        L.ora_neo_stress.argtypes = [ctypes.c_int, P, ctypes.c_double, ctypes.c_double, P]
         L.ora_assemble_residual.argtypes = [ctypes.POINTER(_Mesh), ctypes.c_int, P, P, P, P, P, ctypes.c_int, P]
         L.ora_apply_lifting.argtypes = [ctypes.POINTER(_Mesh), ctypes.c_int, P, P, P, P, ctypes.c_int, P, P, P,
                                         ctypes.c_double, P]
@@ -230,7 +231,8 @@ def _opt(a, dtype=np.float64):
 
 
 def assemble_residual(cell_type, degree, cells, geom, x, lam, mu, u=None, f=None, d=None, kind=0, qdeg=-1):
-    """dolfinx assemble_vector of inner(sigma(u), eps(v)) dxx - inner(f, v) dx (kind 1: damage law)."""
+    """dolfinx assemble_vector of inner(sigma(u), eps(v)) dxx - inner(f, v) dx (kind 1: damage law;
+    kind 2: neo-Hookean, sigma -> first Piola stress)."""
     cells = np.ascontiguousarray(cells, dtype=np.int32)
     geom = np.ascontiguousarray(geom, dtype=np.int32)
     x = np.ascontiguousarray(x, dtype=np.float64)
@@ -302,3 +304,12 @@ def neo_tangent(F, lam, mu):
     A = np.zeros((gd * gd, gd * gd))
     lib().ora_neo_tangent(gd, _p(F), lam, mu, _p(A))
     return A
+
+
+def neo_stress(F, lam, mu):
+    """First Piola stress of the neo-Hookean potential (closed form), [gd, gd]."""
+    F = np.ascontiguousarray(F, dtype=np.float64)
+    gd = F.shape[0]
+    P = np.zeros((gd, gd))
+    lib().ora_neo_stress(gd, _p(F), lam, mu, _p(P))
+    return P

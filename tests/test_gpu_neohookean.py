@@ -75,3 +75,33 @@ def test_neohookean_reduces_to_linear_at_zero_state(oracle, dev):
     lin = fem.LinearElasticity(V, E=a.E, nu=0.3)
     A2 = fem.assemble_matrix(lin)
     assert ((A2.data - d1).abs().max() <= RTOL * d1.abs().max()).item()
+
+
+@pytest.mark.parametrize("ct,p,n", CASES)
+def test_residual_matches_oracle(oracle, dev, ct, p, n):
+    """Neo-Hookean residual (first Piola stress by device AD) vs the oracle's closed form."""
+    from femasm import fem
+
+    m, V, a = _setup(oracle, ct, p, n, dev)
+    b = fem.assemble_vector(a)
+    lam, mu = oracle.lame(_np(a.E), 0.3)
+    ref = oracle.assemble_residual(ct, p, _np(V.dofmap), _np(m.cells), _np(m.x), lam, mu, u=_np(a.u), kind=2)
+    assert np.abs(_np(b) - ref).max() <= RTOL * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("ct,p,n", CASES)
+def test_lifting_matches_oracle(oracle, dev, ct, p, n):
+    """apply_lifting with the neo-Hookean tangent at the state (dolfinx semantics, alpha = -1)."""
+    from femasm import fem
+
+    m, V, a = _setup(oracle, ct, p, n, dev)
+    right = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.ones_like(x[0])))
+    bcs = [fem.dirichletbc([0.02] + [0.0] * (m.gdim - 1), right, V)]
+    b = torch.zeros(V.num_dofs, dtype=torch.float64, device=dev)
+    fem.apply_lifting(b, [a], [bcs], x0=[a.u], alpha=-1.0)
+    marker, gv = fem._combine_bcs(V, bcs)
+    lam, mu = oracle.lame(_np(a.E), 0.3)
+    ref = oracle.apply_lifting(ct, p, _np(V.dofmap), _np(m.cells), _np(m.x), lam, mu, np.zeros(V.num_dofs),
+                               _np(marker), _np(gv), x0=_np(a.u), alpha=-1.0, u=_np(a.u), kind=2)
+    assert np.abs(ref).max() > 0
+    assert np.abs(_np(b) - ref).max() <= RTOL * np.abs(ref).max()

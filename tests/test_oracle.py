@@ -200,3 +200,50 @@ def test_neo_hookean_tangent_is_hessian(oracle, gd):
     Hn = np.array(H.subs(sub).evalf(30).tolist(), dtype=np.float64)
     A = oracle.neo_tangent(Fn, 1.7, 0.9)
     np.testing.assert_allclose(A, Hn, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("gd", [2, 3])
+def test_neo_hookean_stress_is_gradient(oracle, gd):
+    """The oracle's first Piola stress equals the SymPy gradient of psi(F) (residual of config E)."""
+    Fs = sp.Matrix(gd, gd, lambda i, j: sp.Symbol(f"F{i}{j}", real=True))
+    lam, mu = sp.Rational(17, 10), sp.Rational(9, 10)
+    J = Fs.det()
+    psi = mu / 2 * (sum(v ** 2 for v in Fs) + (1 if gd == 2 else 0) - 3) - mu * sp.log(J) + lam / 2 * sp.log(J) ** 2
+    flat = list(Fs)
+    rng = np.random.default_rng(10 + gd)
+    Fn = np.eye(gd) + 0.1 * rng.uniform(-1, 1, (gd, gd))
+    sub = {flat[k]: Fn.reshape(-1)[k] for k in range(gd * gd)}
+    Pn = np.array([float(sp.diff(psi, v).subs(sub).evalf(30)) for v in flat]).reshape(gd, gd)
+    np.testing.assert_allclose(oracle.neo_stress(Fn, 1.7, 0.9), Pn, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("ct,deg", [(3, 2), (-4, 2)])
+def test_neo_hookean_residual_tangent_consistent(oracle, ct, deg):
+    """Assembled neo-Hookean residual r(u) and tangent K(u): K du matches the central difference
+    of r (the Newton driver's consistency requirement), on a small perturbed mesh."""
+    from femasm import mesh as fmesh
+    from femasm import fem
+
+    m = (fmesh.create_unit_square(2, 2, fmesh.CellType.triangle) if ct == 3
+         else fmesh.create_unit_cube(1, 1, 2, fmesh.CellType.tetrahedron))
+    V = fem.functionspace(m, ("Lagrange", deg, (m.gdim,)))
+    cells = V.dofmap.cpu().numpy()
+    xn = V.tabulate_dof_coordinates().cpu().numpy()
+    geom = m.cells.cpu().numpy()
+    x = m.x.cpu().numpy()
+    rng = np.random.default_rng(4)
+    u = 0.01 * rng.standard_normal(xn.shape[0] * m.gdim)
+    du = rng.standard_normal(u.shape)
+    lam, mu = 1.3, 0.7
+    nn = cells.shape[1]
+    Ae = oracle.assemble_neohookean(ct, deg, cells, geom, x, lam, mu, u, cell_matrices=True)
+    Kdu = np.zeros_like(u)
+    bs = m.gdim
+    for c in range(cells.shape[0]):
+        dofs = (cells[c][:, None] * bs + np.arange(bs)[None, :]).reshape(-1)
+        Kdu[dofs] += Ae[c] @ du[dofs]
+    h = 1e-6
+    rp = oracle.assemble_residual(ct, deg, cells, geom, x, lam, mu, u=u + h * du, kind=2)
+    rm = oracle.assemble_residual(ct, deg, cells, geom, x, lam, mu, u=u - h * du, kind=2)
+    np.testing.assert_allclose((rp - rm) / (2 * h), Kdu, rtol=1e-6, atol=1e-7 * np.abs(Kdu).max())
+    assert nn == cells.shape[1]
