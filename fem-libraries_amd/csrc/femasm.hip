@@ -850,6 +850,8 @@ struct GatherArgs {
   const int64_t* adj_ptr;
   const int32_t* adj_idx;
   const int64_t* row_start;
+  const int64_t* chunk_b;  // [nchunks + 1] indptr[row_start[c]] (k_chunk_desc)
+  const int64_t* chunk_a;  // [nchunks + 1] adj_ptr[row_start[c]]
   int64_t nchunks;
   const uint16_t* slots;  // optional [adjacency entry][NN] position of the block within its row
   const int8_t* bc;
@@ -973,16 +975,59 @@ __device__ __forceinline__ int lds_find(const int32_t* cols, int lo, int hi, int
   return -1;
 }
 
+// Position of `col` in the sorted cols[lo, hi): fixed-trip lower bound (niter = ceil(log2) of the
+// chunk's longest row, wave-uniform), so lanes of different rows do not diverge; -1 if absent.
+__device__ __forceinline__ int lds_slot(const int32_t* cols, int lo, int hi, int32_t col, int niter) {
+  int l = lo, n = hi - lo;
+  for (int k = 0; k < niter; ++k) {
+    const int h = n >> 1;
+    const int32_t cv = cols[l + h];  // unconditional read (in the chunk's slots): no branch
+    l = ((h > 0) & (cv <= col)) ? l + h : l;
+    n -= h;
+  }
+  const int32_t cv = cols[l];
+  return ((n > 0) & (cv == col)) ? l : -1;
+}
+
+// Add a GD x GD block into LDS slot s. rowm/colm: the constrained-dof bits of the block's row
+// and column node (zero for almost every block: then no per-entry test).
+template <int GD>
+__device__ __forceinline__ void lds_add_block(double* acc, int s, const double (&K)[GD][GD], uint32_t rowm,
+                                              uint32_t colm) {
+  constexpr int BS2 = GD * GD;
+  if ((rowm | colm) == 0u) {
+#pragma unroll
+    for (int i = 0; i < GD; ++i)
+#pragma unroll
+      for (int jj = 0; jj < GD; ++jj) atomicAdd(&acc[s * BS2 + i * GD + jj], K[i][jj]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < GD; ++i)
+#pragma unroll
+      for (int jj = 0; jj < GD; ++jj)
+        if (!((rowm >> i) & 1u) && !((colm >> jj) & 1u)) atomicAdd(&acc[s * BS2 + i * GD + jj], K[i][jj]);
+  }
+}
+
 // Items are (adjacency entry, column-node group). NSPLIT groups split the cell's NN column
 // nodes so that a chunk exposes enough independent items to all 256 lanes.
 #ifndef FA_GATHER_WAVES
 #define FA_GATHER_WAVES 4  // min waves per SIMD: 4 -> <= 128 VGPRs (16 waves / CU); measured best
 #endif
 #ifndef FA_GATHER_PERMUTE
-#define FA_GATHER_PERMUTE 1  // measured +4 % on config E (fewer same-slot LDS adds per instruction)
+#define FA_GATHER_PERMUTE 1  // measured +16 % on config E at n = 120 (fewer same-slot LDS adds per instruction)
 #endif
 #ifndef FA_GATHER_UNROLL_B
 #define FA_GATHER_UNROLL_B 1
+#endif
+// Timing-only ablations of the affine-simplex gather (wrong results; tools/ablate.sh):
+// 1 early-exit search, 2 no search, 3 no LDS adds, 4 no reference-tensor LDS reads,
+// 5 no block arithmetic, 6 no item loop (chunk setup + store only), 7 no per-item global loads
+#ifndef FA_ABL
+#define FA_ABL 0
+#endif
+#ifndef FA_GATHER_PIPE_NEO
+#define FA_GATHER_PIPE_NEO 0
 #endif
 template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT>
 __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
@@ -991,8 +1036,9 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   constexpr int MAXB = kGatherLdsValues / (8 * BS2);
   constexpr bool SIMP = R::SIMP;
   constexpr int NBG = (NN + NSPLIT - 1) / NSPLIT;  // column nodes per item
-  __shared__ double acc[MAXB * BS2];
+  __shared__ double acc[(MAXB + 1) * BS2];  // + one sink slot for (erroneous) missing columns
   __shared__ int32_t cols[MAXB];
+  __shared__ int s_maxrow;
   __shared__ int32_t rowoff[kGatherMaxRows + 1];
   __shared__ uint8_t adjrow[kGatherMaxAdj];
   constexpr bool NEO = (MAT == FA_NEO_HOOKEAN);
@@ -1001,29 +1047,25 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   __shared__ double s_dphi[TAB ? NQ * NN * GD : 1];
   __shared__ double s_ahat[SIMP ? NN * NN * BS2 : 1];
 
-  // XCD-aware chunk order: blocks b and b+8 share an XCD (round-robin dispatch), so XCD
-  // (b % 8) walks the contiguous chunk range [(b % 8) * per, (b % 8 + 1) * per).
-  const int64_t per = (P.nchunks + 7) / 8;
-  for (int64_t vb = blockIdx.x; vb < 8 * per; vb += gridDim.x) {  // gridDim.x % 8 == 0: vb % 8 == blockIdx.x % 8
-  const int64_t chunk = (vb % 8) * per + vb / 8;
-  if (chunk >= P.nchunks) continue;
-  __syncthreads();  // LDS reuse across iterations
-
   const int tid = threadIdx.x;
-  const int64_t r0 = P.row_start[chunk], r1 = P.row_start[chunk + 1];
-  const int nrows = (int)(r1 - r0);
-  const int64_t b0 = P.A.indptr[r0], b1 = P.A.indptr[r1];
-  const int nb = (int)(b1 - b0);
-  const int64_t a0 = P.adj_ptr[r0], a1 = P.adj_ptr[r1];
-  const int na = (int)(a1 - a0);
+  constexpr int NPC = (MAXB + 255) / 256;           // column indices per thread (metadata slice)
+  constexpr int NPA = (kGatherMaxAdj + 255) / 256;  // adjacency entries per thread
+  static_assert(kGatherMaxRows < 256, "one row offset per thread");
+  __shared__ int32_t s_adj[kGatherMaxAdj];
 
-  for (int t = tid; t < nb * BS2; t += 256) acc[t] = 0.0;
-  for (int t = tid; t < nb; t += 256) cols[t] = P.A.indices[b0 + t];
-  for (int t = tid; t <= nrows; t += 256) rowoff[t] = (int)(P.A.indptr[r0 + t] - b0);
-  for (int t = tid; t < nrows; t += 256) {
-    int64_t j0 = P.adj_ptr[r0 + t], j1 = P.adj_ptr[r0 + t + 1];
-    for (int64_t j = j0; j < j1; ++j) adjrow[j - a0] = (uint8_t)t;
-  }
+  // XCD-aware chunk order: blocks b and b+8 share an XCD (round-robin dispatch), so XCD
+  // (b % 8) walks the contiguous chunk range [(b % 8) * per, (b % 8 + 1) * per). A workgroup's
+  // valid chunks are a prefix of its sequence vb = blockIdx.x + k * gridDim.x.
+  const int64_t per = (P.nchunks + 7) / 8;
+  const int64_t vstep = gridDim.x;  // gridDim.x % 8 == 0: vb % 8 == blockIdx.x % 8
+  auto chunk_of = [&](int64_t v) -> int64_t {
+    if (v >= 8 * per) return P.nchunks;
+    const int64_t c = (v % 8) * per + v / 8;
+    return c < P.nchunks ? c : P.nchunks;
+  };
+  int64_t vb = blockIdx.x;
+  if (chunk_of(vb) >= P.nchunks) return;  // whole workgroup idle
+
   if constexpr (MAT == MAT_BLOCKS) {
   } else if constexpr (NEO) {
     for (int t = tid; t < NQ; t += 256) s_w[t] = P.tab[t];
@@ -1034,23 +1076,112 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     for (int t = tid; t < NQ; t += 256) s_w[t] = P.tab[t];
     for (int t = tid; t < NQ * NN * GD; t += 256) s_dphi[t] = P.tab[NQ + t];
   }
+
+  // Software pipeline over the workgroup's chunks: while chunk k is assembled, the metadata of
+  // chunk k+1 (its column indices, row offsets, adjacency) is in flight into registers and the
+  // descriptor of chunk k+2 is loaded, so a chunk starts with one exposed latency (its cells'
+  // records) instead of four dependent ones (measured: the un-pipelined skeleton alone took
+  // 46 of 84 ms on config E, tools/ablate.sh FA_ABL=6).
+  struct Desc { int64_t r0, r1, b0, b1, a0, a1; };
+  auto load_desc = [&](int64_t c) -> Desc {
+    return Desc{P.row_start[c], P.row_start[c + 1], P.chunk_b[c], P.chunk_b[c + 1], P.chunk_a[c], P.chunk_a[c + 1]};
+  };
+  int32_t pc[NPC], pj[NPA];
+  // row / adjacency pointers: low 32 bits only (differences within a chunk are < 2^31)
+  uint32_t prow = 0, pa0 = 0, pa1 = 0;
+  const uint32_t* indptr_lo = reinterpret_cast<const uint32_t*>(P.A.indptr);
+  const uint32_t* adjptr_lo = reinterpret_cast<const uint32_t*>(P.adj_ptr);
+  auto fetch = [&](const Desc& d) {
+    const int nb_ = (int)(d.b1 - d.b0), nr_ = (int)(d.r1 - d.r0), na_ = (int)(d.a1 - d.a0);
+#pragma unroll
+    for (int k = 0; k < NPC; ++k) {
+      const int t = tid + 256 * k;
+      pc[k] = t < nb_ ? P.A.indices[d.b0 + t] : 0;
+    }
+    prow = tid <= nr_ ? indptr_lo[2 * (d.r0 + tid)] : 0u;
+    pa0 = tid < nr_ ? adjptr_lo[2 * (d.r0 + tid)] : 0u;
+    pa1 = tid < nr_ ? adjptr_lo[2 * (d.r0 + tid + 1)] : 0u;
+#pragma unroll
+    for (int k = 0; k < NPA; ++k) {
+      const int t = tid + 256 * k;
+      pj[k] = t < na_ ? P.adj_idx[d.a0 + t] : 0;
+    }
+  };
+  auto stage = [&](const Desc& d) {  // registers -> LDS, accumulator zeroed
+    const int nb_ = (int)(d.b1 - d.b0), nr_ = (int)(d.r1 - d.r0), na_ = (int)(d.a1 - d.a0);
+    for (int t = tid; t < nb_ * BS2; t += 256) acc[t] = 0.0;
+#pragma unroll
+    for (int k = 0; k < NPC; ++k) {
+      const int t = tid + 256 * k;
+      if (t < nb_) cols[t] = pc[k];
+    }
+    if (tid <= nr_) rowoff[tid] = (int)(prow - (uint32_t)d.b0);
+    if (tid < nr_) {
+      const int j0 = (int)(pa0 - (uint32_t)d.a0), j1 = (int)(pa1 - (uint32_t)d.a0);
+      for (int j = j0; j < j1; ++j) adjrow[j] = (uint8_t)tid;
+    }
+#pragma unroll
+    for (int k = 0; k < NPA; ++k) {
+      const int t = tid + 256 * k;
+      if (t < na_) s_adj[t] = pj[k];
+    }
+    if (tid == 0) s_maxrow = 1;
+  };
+
+  // neo-Hookean items hold large per-q tangents: the prefetch registers would spill there
+  constexpr bool PIPE = !NEO || FA_GATHER_PIPE_NEO;
+  Desc cur = load_desc(chunk_of(vb));
+  fetch(cur);
+  stage(cur);
+  int64_t nchunk = chunk_of(vb + vstep);
+  Desc nxt = nchunk < P.nchunks ? load_desc(nchunk) : cur;
   __syncthreads();
+  for (;;) {
+  if (PIPE && nchunk < P.nchunks) fetch(nxt);  // lands while this chunk is assembled
+  const int64_t nnchunk = chunk_of(vb + 2 * vstep);
+  const Desc nn2 = nnchunk < P.nchunks ? load_desc(nnchunk) : nxt;
+
+  const int64_t r0 = cur.r0;
+  const int nrows = (int)(cur.r1 - cur.r0);
+  const int64_t b0 = cur.b0;
+  const int nb = (int)(cur.b1 - cur.b0);
+  const int64_t a0 = cur.a0;
+  const int na = (int)(cur.a1 - cur.a0);
+  for (int t = tid; t < nrows; t += 256) atomicMax(&s_maxrow, rowoff[t + 1] - rowoff[t]);
+  __syncthreads();
+  const int niter = 32 - __clz(s_maxrow);  // >= ceil(log2(maxrow)) + 0/1 halvings to reach n == 1
+  int bad = 0;
+#if FA_ABL == 3
+  double abl_sink = 0.0;
+#endif
 
   const int nitems = na * NSPLIT;
-#if FA_GATHER_PERMUTE
-  // consecutive items belong to the same row and add into the same LDS slots (the diagonal
-  // block of a vertex row gets ~24 adds); a stride coprime to nitems spreads rows over lanes
+  // (neo-Hookean: measured 3 % faster without the permutation, n = 120)
+  constexpr bool PERM = FA_GATHER_PERMUTE && !NEO;
+  // consecutive adjacency entries belong to the same row and add into the same LDS slots (the
+  // diagonal block of a vertex row gets ~24 adds); a stride coprime to na spreads rows over
+  // lanes. The NSPLIT parts of one entry stay on neighbouring lanes (they read the same cell
+  // record). (jp * stride) mod na in 32-bit with a float quotient estimate (x < 2^24: off by <= 1).
   int stride = 97;
-  while (nitems % stride == 0 && stride > 1) stride -= 2;
-#endif
-  for (int it0 = tid; it0 < nitems; it0 += 256) {
-#if FA_GATHER_PERMUTE
-    const int it = (int)(((int64_t)it0 * stride) % nitems);
+  while (PERM && na % stride == 0 && stride > 1) stride -= 2;
+  const float inv_n = 1.0f / (float)na;
+#if FA_ABL == 6
+  for (int it0 = tid; it0 < 0; it0 += 256) {
 #else
-    const int it = it0;
+  for (int it0 = tid; it0 < nitems; it0 += 256) {
 #endif
-    const int j = it / NSPLIT, part = it % NSPLIT;
-    const int32_t pflat = P.adj_idx[a0 + j];
+    const int part = it0 % NSPLIT;
+    int j = it0 / NSPLIT;
+    if constexpr (PERM) {
+      const int x = j * stride;
+      j = x - na * (int)((float)x * inv_n);
+      j = j < 0 ? j + na : (j >= na ? j - na : j);
+    }
+#if FA_ABL == 7
+    const int32_t pflat = (int32_t)((r0 + j) * 7 % (P.M.ncells * NN));
+#else
+    const int32_t pflat = s_adj[j];
+#endif
     const int64_t c = pflat / NN;
     const int aloc = pflat % NN;
     const int lr = adjrow[j];
@@ -1059,6 +1190,14 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     // registers: NEO keeps only Ji, wdet; tensor cells read their per-q records in the q loop
     constexpr int RL = NEO ? ((BS2 + 2) & ~1) : (SIMP || MAT == FA_ASYM_DAMAGE ? R::SIZE : 2);
     double r[RL];
+#if FA_ABL == 7
+#pragma unroll
+    for (int k = 0; k < RL; ++k) r[k] = 0.5 + 0.01 * k + 1e-9 * (double)c;
+    int32_t cn[NBG];
+#pragma unroll
+    for (int bb = 0; bb < NBG; ++bb) cn[bb] = cols[lo + (int)((c + bb) % (hi - lo))];
+    const uint32_t mask = 0u;
+#else
     if constexpr (MAT != MAT_BLOCKS) {
       const double2* rp = reinterpret_cast<const double2*>(P.rec + c * R::SIZE);
 #pragma unroll
@@ -1075,6 +1214,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       cn[bb] = b < NN ? P.M.cells[c * NN + b] : -1;
     }
     const uint32_t mask = P.bcmask ? P.bcmask[c] : 0u;
+#endif
 
     if constexpr (MAT == MAT_BLOCKS) {
       const double* Eb = P.rec + ((int64_t)c * NN + aloc) * NN * BS2;  // bc already applied
@@ -1082,8 +1222,9 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       for (int bb = 0; bb < NBG; ++bb) {
         const int b = part * NBG + bb;
         if (b >= NN) break;
-        const int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_find(cols, lo, hi, cn[bb]);
-        if (s < 0) { atomicOr(P.err, 1); continue; }
+        int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_slot(cols, lo, hi, cn[bb], niter);
+        bad |= s < 0;
+        s = s < 0 ? MAXB : s;
 #pragma unroll
         for (int e = 0; e < BS2; ++e) atomicAdd(&acc[s * BS2 + e], Eb[b * BS2 + e]);
       }
@@ -1102,14 +1243,10 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
         double gb[2] = {r[2 * b], r[2 * b + 1]};
         double K[2][2];
         damage_block(ga, gb, w, H, K);
-        const int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_find(cols, lo, hi, cn[bb]);
-        if (s < 0) { atomicOr(P.err, 1); continue; }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
-            if (!((mask >> (aloc * 2 + i)) & 1u) && !((mask >> (b * 2 + jj)) & 1u))
-              atomicAdd(&acc[s * 4 + i * 2 + jj], K[i][jj]);
+        int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_slot(cols, lo, hi, cn[bb], niter);
+        bad |= s < 0;
+        s = s < 0 ? MAXB : s;
+        lds_add_block<2>(acc, s, K, (mask >> (aloc * 2)) & 3u, (mask >> (b * 2)) & 3u);
       }
     } else if constexpr (NEO) {
       // K_ab[i][k] = sum_q w_q |J| sum_{J,L} ga_q[J] A_q[(iJ)(kL)] gb_q[L]; per q the row node's
@@ -1178,14 +1315,10 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       for (int bb = 0; bb < NBG; ++bb) {
         const int b = part * NBG + bb;
         if (b >= NN) break;
-        const int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_find(cols, lo, hi, cn[bb]);
-        if (s < 0) { atomicOr(P.err, 1); continue; }
-#pragma unroll
-        for (int i = 0; i < GD; ++i)
-#pragma unroll
-          for (int jj = 0; jj < GD; ++jj)
-            if (!((mask >> (aloc * GD + i)) & 1u) && !((mask >> (b * GD + jj)) & 1u))
-              atomicAdd(&acc[s * BS2 + i * GD + jj], K[bb][i][jj]);
+        int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_slot(cols, lo, hi, cn[bb], niter);
+        bad |= s < 0;
+        s = s < 0 ? MAXB : s;
+        lds_add_block<GD>(acc, s, K[bb], (mask >> (aloc * GD)) & ((1u << GD) - 1), (mask >> (b * GD)) & ((1u << GD) - 1));
       }
     } else if constexpr (SIMP) {
       // affine simplex: G_ab = |J| Ji^T Ahat_ab Ji  (reference-tensor form)
@@ -1194,7 +1327,14 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       for (int bb = 0; bb < NBG; ++bb) {
         const int b = part * NBG + bb;
         if (b >= NN) break;
+#if FA_ABL == 4
+        double Ahr[BS2];
+#pragma unroll
+        for (int e = 0; e < BS2; ++e) Ahr[e] = 0.1 * (e + aloc) + b;
+        const double* Ah = Ahr;
+#else
         const double* Ah = s_ahat + (aloc * NN + b) * BS2;
+#endif
         double T[GD][GD];  // T = Ahat Ji
 #pragma unroll
         for (int i = 0; i < GD; ++i)
@@ -1216,15 +1356,31 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
             G[e][d] = g;
           }
         double K[GD][GD];
-        lin_block<GD>(G, lam, mu, K);
-        const int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_find(cols, lo, hi, cn[bb]);
-        if (s < 0) { atomicOr(P.err, 1); continue; }
+#if FA_ABL == 5
 #pragma unroll
         for (int i = 0; i < GD; ++i)
 #pragma unroll
-          for (int jj = 0; jj < GD; ++jj)
-            if (!((mask >> (aloc * GD + i)) & 1u) && !((mask >> (b * GD + jj)) & 1u))
-              atomicAdd(&acc[s * BS2 + i * GD + jj], K[i][jj]);
+          for (int jj = 0; jj < GD; ++jj) K[i][jj] = r[i * GD + jj] * lam + Ah[0] * mu;
+#else
+        lin_block<GD>(G, lam, mu, K);
+#endif
+#if FA_ABL == 1
+        int s = lds_find(cols, lo, hi, cn[bb]);
+#elif FA_ABL == 2
+        int s = lo + (int)((uint32_t)cn[bb] % (uint32_t)(hi - lo));
+#else
+        int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_slot(cols, lo, hi, cn[bb], niter);
+#endif
+        bad |= s < 0;
+        s = s < 0 ? MAXB : s;
+#if FA_ABL == 3
+#pragma unroll
+        for (int i = 0; i < GD; ++i)
+#pragma unroll
+          for (int jj = 0; jj < GD; ++jj) abl_sink += K[i][jj] * (double)s;
+#else
+        lds_add_block<GD>(acc, s, K, (mask >> (aloc * GD)) & ((1u << GD) - 1), (mask >> (b * GD)) & ((1u << GD) - 1));
+#endif
       }
     } else {
       // non-affine tensor cells: J^-1 per quadrature point, read from the record as the rolled
@@ -1278,17 +1434,17 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
         if (b >= NN) break;
         double K[GD][GD];
         lin_block<GD>(G[bb], lam, mu, K);
-        const int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_find(cols, lo, hi, cn[bb]);
-        if (s < 0) { atomicOr(P.err, 1); continue; }
-#pragma unroll
-        for (int i = 0; i < GD; ++i)
-#pragma unroll
-          for (int jj = 0; jj < GD; ++jj)
-            if (!((mask >> (aloc * GD + i)) & 1u) && !((mask >> (b * GD + jj)) & 1u))
-              atomicAdd(&acc[s * BS2 + i * GD + jj], K[i][jj]);
+        int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_slot(cols, lo, hi, cn[bb], niter);
+        bad |= s < 0;
+        s = s < 0 ? MAXB : s;
+        lds_add_block<GD>(acc, s, K, (mask >> (aloc * GD)) & ((1u << GD) - 1), (mask >> (b * GD)) & ((1u << GD) - 1));
       }
     }
   }
+#if FA_ABL == 3
+  if (abl_sink == 1.2345) acc[0] = abl_sink;
+#endif
+  if (bad) atomicOr(P.err, 1);
   __syncthreads();
   if (P.bc) {
     for (int t = tid; t < nrows * GD; t += 256) {
@@ -1303,6 +1459,15 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   }
   double* out = P.A.data + (b0 - P.A.indptr[P.A.row_begin]) * BS2;
   for (int t = tid; t < nb * BS2; t += 256) out[t] = acc[t];
+  if (nchunk >= P.nchunks) break;
+  __syncthreads();  // the store has read acc
+  if (!PIPE) fetch(nxt);
+  stage(nxt);
+  cur = nxt;
+  nxt = nn2;
+  nchunk = nnchunk;
+  vb += vstep;
+  __syncthreads();
   }
 }
 
@@ -1631,6 +1796,27 @@ static int scratch_alloc(void** p, size_t bytes, hipStream_t s) {
   return FA_OK;
 }
 
+// per-chunk block / adjacency offsets: one dependent load level less in the gather's pipeline
+__global__ void k_chunk_desc(const int64_t* __restrict__ row_start, int64_t nchunks, const int64_t* __restrict__ indptr,
+                             const int64_t* __restrict__ adj_ptr, int64_t* __restrict__ cb, int64_t* __restrict__ ca) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c <= nchunks; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = row_start[c];
+    cb[c] = indptr[r];
+    ca[c] = adj_ptr[r];
+  }
+}
+
+static int chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
+  int rc;
+  if ((rc = scratch_alloc((void**)buf, sizeof(int64_t) * 2 * (P.nchunks + 1), s))) return rc;
+  P.chunk_b = *buf;
+  P.chunk_a = *buf + (P.nchunks + 1);
+  k_chunk_desc<<<grid_for(P.nchunks + 1), 256, 0, s>>>(P.row_start, P.nchunks, P.A.indptr, P.adj_ptr, *buf,
+                                                      *buf + (P.nchunks + 1));
+  LAUNCH_CHECK();
+  return FA_OK;
+}
+
 template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT>
 static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s) {
   using R = Rec<GD, NV, NQ, MAT>;
@@ -1648,10 +1834,13 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s) {
   P.rec = rec;
   P.bcmask = mask;
   if (P.nchunks > 0) {
+    int64_t* desc = nullptr;
+    if ((rc = chunk_desc(P, &desc, s))) return rc;
     const int64_t per = (P.nchunks + 7) / 8;
     const int64_t grid = std::min<int64_t>(8 * per, kMaxBlocks);  // kMaxBlocks % 8 == 0
     k_gather<GD, NN, NV, NQ, NSPLIT, MAT><<<(unsigned)grid, 256, 0, s>>>(P);
     LAUNCH_CHECK();
+    HIP_TRY(hipFreeAsync(desc, s));
   }
   HIP_TRY(hipFreeAsync(rec, s));
   if (mask) HIP_TRY(hipFreeAsync(mask, s));
@@ -1682,10 +1871,13 @@ static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc,
   P.rec = eb;
   P.bcmask = nullptr;
   if (P.nchunks > 0) {
+    int64_t* desc = nullptr;
+    if ((rc = chunk_desc(P, &desc, s))) return rc;
     const int64_t per = (P.nchunks + 7) / 8;
     const int64_t grid = std::min<int64_t>(8 * per, kMaxBlocks);
     k_gather<3, NN, 8, NQ, NSPLIT, MAT_BLOCKS><<<(unsigned)grid, 256, 0, s>>>(P);
     LAUNCH_CHECK();
+    HIP_TRY(hipFreeAsync(desc, s));
   }
   HIP_TRY(hipFreeAsync(eb, s));
   return FA_OK;
