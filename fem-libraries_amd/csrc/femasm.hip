@@ -18,12 +18,15 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <map>
 #include <mutex>
 #include <string>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/femasm.h"
@@ -279,13 +282,15 @@ __device__ __forceinline__ void phys_grad(const double* dphi, const double (&Ji)
 // K_ab[i][j] = lam G[i][j] + mu G[j][i] + mu tr(G) delta_ij
 template <int GD>
 __device__ __forceinline__ void lin_block(const double (&G)[GD][GD], double lam, double mu, double (&K)[GD][GD]) {
-  double tr = 0.0;
+  // K = lam G + mu G^T + mu tr(G) I, written without "+ 0.0" terms (the compiler must keep those)
+  double tr = G[0][0];
 #pragma unroll
-  for (int i = 0; i < GD; ++i) tr += G[i][i];
+  for (int i = 1; i < GD; ++i) tr += G[i][i];
+  const double mtr = mu * tr, lm = lam + mu;
 #pragma unroll
   for (int i = 0; i < GD; ++i)
 #pragma unroll
-    for (int j = 0; j < GD; ++j) K[i][j] = lam * G[i][j] + mu * G[j][i] + (i == j ? mu * tr : 0.0);
+    for (int j = 0; j < GD; ++j) K[i][j] = (i == j) ? fma(lm, G[i][i], mtr) : fma(mu, G[j][i], lam * G[i][j]);
 }
 
 // Reference damage-law tangent "hook" (Voigt xx, yy, xy-engineering), restated from MFEM
@@ -989,24 +994,51 @@ __device__ __forceinline__ int lds_slot(const int32_t* cols, int lo, int hi, int
   return ((n > 0) & (cv == col)) ? l : -1;
 }
 
+// lds_slot for NB columns of ONE row at once: the searches share the interval length, so the
+// NB probes of each halving step are independent LDS reads issued together (one latency per
+// step instead of NB).
+template <int NB>
+__device__ __forceinline__ void lds_slots(const int32_t* cols, int lo, int hi, const int32_t (&col)[NB], int niter,
+                                          int (&sl)[NB]) {
+  int n = hi - lo;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) sl[b] = lo;
+  for (int k = 0; k < niter; ++k) {
+    const int h = n >> 1;
+    int32_t cv[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) cv[b] = cols[sl[b] + h];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) sl[b] = ((h > 0) & (cv[b] <= col[b])) ? sl[b] + h : sl[b];
+    n -= h;
+  }
+  int32_t cv[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) cv[b] = cols[sl[b]];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) sl[b] = ((n > 0) & (cv[b] == col[b])) ? sl[b] : -1;
+}
+
 // Add a GD x GD block into LDS slot s. rowm/colm: the constrained-dof bits of the block's row
 // and column node (zero for almost every block: then no per-entry test).
 template <int GD>
-__device__ __forceinline__ void lds_add_block(double* acc, int s, const double (&K)[GD][GD], uint32_t rowm,
+__device__ __forceinline__ void lds_add_block(double* acc, int s, double (&K)[GD][GD], uint32_t rowm,
                                               uint32_t colm) {
-  constexpr int BS2 = GD * GD;
-  if ((rowm | colm) == 0u) {
-#pragma unroll
-    for (int i = 0; i < GD; ++i)
-#pragma unroll
-      for (int jj = 0; jj < GD; ++jj) atomicAdd(&acc[s * BS2 + i * GD + jj], K[i][jj]);
-  } else {
+  // Constrained entries are zeroed (only in waves that hold one: a wave-uniform branch), then all
+  // GD^2 adds are issued unconditionally. An add of 0.0 into a constrained diagonal entry that
+  // another lane sets to `diag` concurrently is harmless: LDS atomics are indivisible, and
+  // diag + 0.0 == diag.
+  if (__any((rowm | colm) != 0u)) {
 #pragma unroll
     for (int i = 0; i < GD; ++i)
 #pragma unroll
       for (int jj = 0; jj < GD; ++jj)
-        if (!((rowm >> i) & 1u) && !((colm >> jj) & 1u)) atomicAdd(&acc[s * BS2 + i * GD + jj], K[i][jj]);
+        if (((rowm >> i) | (colm >> jj)) & 1u) K[i][jj] = 0.0;
   }
+#pragma unroll
+  for (int i = 0; i < GD; ++i)
+#pragma unroll
+    for (int jj = 0; jj < GD; ++jj) atomicAdd(&acc[s * (GD * GD) + i * GD + jj], K[i][jj]);
 }
 
 // Items are (adjacency entry, column-node group). NSPLIT groups split the cell's NN column
@@ -1021,10 +1053,16 @@ __device__ __forceinline__ void lds_add_block(double* acc, int s, const double (
 #define FA_GATHER_UNROLL_B 1
 #endif
 // Timing-only ablations of the affine-simplex gather (wrong results; tools/ablate.sh):
-// 1 early-exit search, 2 no search, 3 no LDS adds, 4 no reference-tensor LDS reads,
-// 5 no block arithmetic, 6 no item loop (chunk setup + store only), 7 no per-item global loads
+// 3 no LDS adds, 6 no item loop (chunk setup + store only), 7 no per-item global loads,
+// 8 no chunk store, 9 no record loads (column ids and bc mask still loaded)
 #ifndef FA_ABL
 #define FA_ABL 0
+#endif
+#ifndef FA_GATHER_CN_ALWAYS
+#define FA_GATHER_CN_ALWAYS 0
+#endif
+#ifndef FA_GATHER_IPF
+#define FA_GATHER_IPF 0  // affine simplices: the next chunk's first item loaded during this chunk's tail
 #endif
 #ifndef FA_GATHER_PIPE_NEO
 #define FA_GATHER_PIPE_NEO 0
@@ -1040,6 +1078,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   __shared__ int32_t cols[MAXB];
   __shared__ int s_maxrow;
   __shared__ int32_t rowoff[kGatherMaxRows + 1];
+  __shared__ uint8_t s_rowbc[kGatherMaxRows];  // constrained-dof bits of each chunk row
   __shared__ uint8_t adjrow[kGatherMaxAdj];
   constexpr bool NEO = (MAT == FA_NEO_HOOKEAN);
   constexpr bool TAB = (MAT != MAT_BLOCKS) && (NEO || !SIMP);  // quadrature tables staged in LDS
@@ -1088,7 +1127,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   };
   int32_t pc[NPC], pj[NPA];
   // row / adjacency pointers: low 32 bits only (differences within a chunk are < 2^31)
-  uint32_t prow = 0, pa0 = 0, pa1 = 0;
+  uint32_t prow = 0, prow1 = 0, pa0 = 0, pa1 = 0, pbc = 0;
   const uint32_t* indptr_lo = reinterpret_cast<const uint32_t*>(P.A.indptr);
   const uint32_t* adjptr_lo = reinterpret_cast<const uint32_t*>(P.adj_ptr);
   auto fetch = [&](const Desc& d) {
@@ -1099,8 +1138,14 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       pc[k] = t < nb_ ? P.A.indices[d.b0 + t] : 0;
     }
     prow = tid <= nr_ ? indptr_lo[2 * (d.r0 + tid)] : 0u;
+    prow1 = tid < nr_ ? indptr_lo[2 * (d.r0 + tid + 1)] : prow;
     pa0 = tid < nr_ ? adjptr_lo[2 * (d.r0 + tid)] : 0u;
     pa1 = tid < nr_ ? adjptr_lo[2 * (d.r0 + tid + 1)] : 0u;
+    pbc = 0u;
+    if (P.bc && tid < nr_) {
+#pragma unroll
+      for (int i = 0; i < GD; ++i) pbc |= (P.bc[(d.r0 + tid) * GD + i] ? 1u : 0u) << i;
+    }
 #pragma unroll
     for (int k = 0; k < NPA; ++k) {
       const int t = tid + 256 * k;
@@ -1109,7 +1154,15 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   };
   auto stage = [&](const Desc& d) {  // registers -> LDS, accumulator zeroed
     const int nb_ = (int)(d.b1 - d.b0), nr_ = (int)(d.r1 - d.r0), na_ = (int)(d.a1 - d.a0);
-    for (int t = tid; t < nb_ * BS2; t += 256) acc[t] = 0.0;
+    {
+      double2* acc2 = reinterpret_cast<double2*>(acc);
+      const int nv2 = (nb_ * BS2 + 1) >> 1;  // acc holds (MAXB + 1) blocks: the odd tail fits
+      for (int t = tid; t < nv2; t += 256) acc2[t] = make_double2(0.0, 0.0);
+    }
+    if (tid < nr_) {
+      s_rowbc[tid] = (uint8_t)pbc;
+      atomicMax(&s_maxrow, (int)(prow1 - prow));  // s_maxrow was reset during the previous store
+    }
 #pragma unroll
     for (int k = 0; k < NPC; ++k) {
       const int t = tid + 256 * k;
@@ -1125,11 +1178,40 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       const int t = tid + 256 * k;
       if (t < na_) s_adj[t] = pj[k];
     }
-    if (tid == 0) s_maxrow = 1;
   };
 
   // neo-Hookean items hold large per-q tangents: the prefetch registers would spill there
   constexpr bool PIPE = !NEO || FA_GATHER_PIPE_NEO;
+  // consecutive adjacency entries belong to the same row and add into the same LDS slots (the
+  // diagonal block of a vertex row gets ~24 adds); a stride coprime to na spreads rows over
+  // lanes. The NSPLIT parts of one entry stay on neighbouring lanes (they read the same cell
+  // record). (jp * stride) mod na in 32-bit with a float quotient estimate (x < 2^24: off by <= 1).
+  // (neo-Hookean: measured 3 % faster without the permutation, n = 120)
+  constexpr bool PERM = FA_GATHER_PERMUTE && !NEO;
+  auto perm_stride = [&](int na_) {
+    int st = 97;
+    while (PERM && na_ % st == 0 && st > 1) st -= 2;
+    return st;
+  };
+  auto perm = [&](int jj, int na_, int st, float inv) {
+    if constexpr (!PERM) return jj;
+    const int x = jj * st;
+    int j_ = x - na_ * (int)((float)x * inv);
+    return j_ < 0 ? j_ + na_ : (j_ >= na_ ? j_ - na_ : j_);
+  };
+  // Item prefetch (affine-simplex records): the first item of a thread in the NEXT chunk is
+  // loaded after this chunk's items, so its latency hides behind the store / stage / barriers
+  // instead of heading the next chunk's critical path. Its adjacency entry is loaded at the top
+  // of this chunk.
+  constexpr bool IPF = FA_GATHER_IPF && SIMP && !NEO && MAT != MAT_BLOCKS && FA_ABL == 0;
+  constexpr int RLP = IPF ? R::SIZE : 2;
+  double pr[RLP];
+  int32_t pcn[NBG];
+  uint32_t pmask = 0u;
+  int32_t pflat_n = 0;
+  bool have_pf = false;
+  if (tid == 0) s_maxrow = 1;
+  __syncthreads();
   Desc cur = load_desc(chunk_of(vb));
   fetch(cur);
   stage(cur);
@@ -1138,6 +1220,11 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   __syncthreads();
   for (;;) {
   if (PIPE && nchunk < P.nchunks) fetch(nxt);  // lands while this chunk is assembled
+  if (IPF && nchunk < P.nchunks) {
+    const int na_n = (int)(nxt.a1 - nxt.a0);
+    if (tid < na_n * NSPLIT)
+      pflat_n = P.adj_idx[nxt.a0 + perm(tid / NSPLIT, na_n, perm_stride(na_n), 1.0f / (float)na_n)];
+  }
   const int64_t nnchunk = chunk_of(vb + 2 * vstep);
   const Desc nn2 = nnchunk < P.nchunks ? load_desc(nnchunk) : nxt;
 
@@ -1147,41 +1234,33 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   const int nb = (int)(cur.b1 - cur.b0);
   const int64_t a0 = cur.a0;
   const int na = (int)(cur.a1 - cur.a0);
-  for (int t = tid; t < nrows; t += 256) atomicMax(&s_maxrow, rowoff[t + 1] - rowoff[t]);
-  __syncthreads();
   const int niter = 32 - __clz(s_maxrow);  // >= ceil(log2(maxrow)) + 0/1 halvings to reach n == 1
   int bad = 0;
+  // Dirichlet diagonals (dolfinx set_diagonal) before the items: no item adds into a constrained
+  // dof's diagonal entry (its row bit masks the add), so this needs no barrier. The block-store
+  // variant adds pre-zeroed entries unmasked and sets them after the items instead.
+  if (MAT != MAT_BLOCKS && P.bc) {
+    for (int t = tid; t < nrows * GD; t += 256) {
+      const int lr = t / GD, i = t % GD;
+      if (!((s_rowbc[lr] >> i) & 1u)) continue;
+      const int s = lds_find(cols, rowoff[lr], rowoff[lr + 1], (int32_t)(r0 + lr));
+      if (s < 0) { atomicOr(P.err, 2); continue; }
+      acc[s * BS2 + i * GD + i] = P.diag;
+    }
+  }
 #if FA_ABL == 3
   double abl_sink = 0.0;
 #endif
 
   const int nitems = na * NSPLIT;
-  // (neo-Hookean: measured 3 % faster without the permutation, n = 120)
-  constexpr bool PERM = FA_GATHER_PERMUTE && !NEO;
-  // consecutive adjacency entries belong to the same row and add into the same LDS slots (the
-  // diagonal block of a vertex row gets ~24 adds); a stride coprime to na spreads rows over
-  // lanes. The NSPLIT parts of one entry stay on neighbouring lanes (they read the same cell
-  // record). (jp * stride) mod na in 32-bit with a float quotient estimate (x < 2^24: off by <= 1).
-  int stride = 97;
-  while (PERM && na % stride == 0 && stride > 1) stride -= 2;
+  const int stride = perm_stride(na);
   const float inv_n = 1.0f / (float)na;
-#if FA_ABL == 6
-  for (int it0 = tid; it0 < 0; it0 += 256) {
-#else
-  for (int it0 = tid; it0 < nitems; it0 += 256) {
-#endif
+  // the item body; FROMPF: the thread's first item, whose loads were issued during the
+  // previous chunk (compile-time flag, so the prefetch registers die at its end)
+  auto item = [&](const int it0, auto FROMPF) {
     const int part = it0 % NSPLIT;
-    int j = it0 / NSPLIT;
-    if constexpr (PERM) {
-      const int x = j * stride;
-      j = x - na * (int)((float)x * inv_n);
-      j = j < 0 ? j + na : (j >= na ? j - na : j);
-    }
-#if FA_ABL == 7
-    const int32_t pflat = (int32_t)((r0 + j) * 7 % (P.M.ncells * NN));
-#else
+    const int j = perm(it0 / NSPLIT, na, stride, inv_n);
     const int32_t pflat = s_adj[j];
-#endif
     const int64_t c = pflat / NN;
     const int aloc = pflat % NN;
     const int lr = adjrow[j];
@@ -1190,15 +1269,26 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     // registers: NEO keeps only Ji, wdet; tensor cells read their per-q records in the q loop
     constexpr int RL = NEO ? ((BS2 + 2) & ~1) : (SIMP || MAT == FA_ASYM_DAMAGE ? R::SIZE : 2);
     double r[RL];
-#if FA_ABL == 7
+#if FA_ABL == 7 || FA_ABL == 9
 #pragma unroll
     for (int k = 0; k < RL; ++k) r[k] = 0.5 + 0.01 * k + 1e-9 * (double)c;
+#endif
+#if FA_ABL == 7
     int32_t cn[NBG];
 #pragma unroll
-    for (int bb = 0; bb < NBG; ++bb) cn[bb] = cols[lo + (int)((c + bb) % (hi - lo))];
+    for (int bb = 0; bb < NBG; ++bb) cn[bb] = cols[lo + (int)((c + bb) & 7)];
     const uint32_t mask = 0u;
 #else
-    if constexpr (MAT != MAT_BLOCKS) {
+    int32_t cn[NBG];
+    uint32_t mask;
+    if constexpr (decltype(FROMPF)::value) {  // prefetched during the previous chunk
+#pragma unroll
+      for (int k = 0; k < RL; ++k) r[k] = pr[k < RLP ? k : 0];
+#pragma unroll
+      for (int bb = 0; bb < NBG; ++bb) cn[bb] = pcn[bb];
+      mask = pmask;
+    } else {
+    if constexpr (MAT != MAT_BLOCKS && FA_ABL != 9) {
       const double2* rp = reinterpret_cast<const double2*>(P.rec + c * R::SIZE);
 #pragma unroll
       for (int k = 0; k < RL / 2; ++k) {
@@ -1207,13 +1297,15 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
         r[2 * k + 1] = v.y;
       }
     }
-    int32_t cn[NBG];
+    if (!P.slots || FA_GATHER_CN_ALWAYS) {  // column node ids: only the in-kernel slot search needs them
 #pragma unroll
-    for (int bb = 0; bb < NBG; ++bb) {
-      const int b = part * NBG + bb;
-      cn[bb] = b < NN ? P.M.cells[c * NN + b] : -1;
+      for (int bb = 0; bb < NBG; ++bb) {
+        const int b = part * NBG + bb;
+        cn[bb] = b < NN ? P.M.cells[c * NN + b] : -1;
+      }
     }
-    const uint32_t mask = P.bcmask ? P.bcmask[c] : 0u;
+    mask = P.bcmask ? P.bcmask[c] : 0u;
+    }
 #endif
 
     if constexpr (MAT == MAT_BLOCKS) {
@@ -1323,26 +1415,28 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     } else if constexpr (SIMP) {
       // affine simplex: G_ab = |J| Ji^T Ahat_ab Ji  (reference-tensor form)
       const double wdet = r[BS2], lam = r[BS2 + 1] * wdet, mu = r[BS2 + 2] * wdet;
+      int sl[NBG];  // slots of the item's column nodes, searched together
+      if (P.slots) {
+#pragma unroll
+        for (int bb = 0; bb < NBG; ++bb)
+          sl[bb] = part * NBG + bb < NN ? lo + (int)P.slots[(a0 + j) * NN + part * NBG + bb] : 0;
+      } else {
+        lds_slots<NBG>(cols, lo, hi, cn, niter, sl);
+      }
+      const uint32_t rowm = (mask >> (aloc * GD)) & ((1u << GD) - 1);
+      const double* Ah = s_ahat + (aloc * NN + part * NBG) * BS2;
 #pragma unroll FA_GATHER_UNROLL_B
       for (int bb = 0; bb < NBG; ++bb) {
         const int b = part * NBG + bb;
-        if (b >= NN) break;
-#if FA_ABL == 4
-        double Ahr[BS2];
-#pragma unroll
-        for (int e = 0; e < BS2; ++e) Ahr[e] = 0.1 * (e + aloc) + b;
-        const double* Ah = Ahr;
-#else
-        const double* Ah = s_ahat + (aloc * NN + b) * BS2;
-#endif
+        if (NN % NSPLIT != 0 && b >= NN) break;
         double T[GD][GD];  // T = Ahat Ji
 #pragma unroll
         for (int i = 0; i < GD; ++i)
 #pragma unroll
           for (int d = 0; d < GD; ++d) {
-            double t = 0.0;
+            double t = Ah[i * GD] * r[d];
 #pragma unroll
-            for (int k = 0; k < GD; ++k) t += Ah[i * GD + k] * r[k * GD + d];
+            for (int k = 1; k < GD; ++k) t = fma(Ah[i * GD + k], r[k * GD + d], t);
             T[i][d] = t;
           }
         double G[GD][GD];  // G = Ji^T T
@@ -1350,27 +1444,16 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
         for (int e = 0; e < GD; ++e)
 #pragma unroll
           for (int d = 0; d < GD; ++d) {
-            double g = 0.0;
+            double g = r[e] * T[0][d];
 #pragma unroll
-            for (int i = 0; i < GD; ++i) g += r[i * GD + e] * T[i][d];
+            for (int i = 1; i < GD; ++i) g = fma(r[i * GD + e], T[i][d], g);
             G[e][d] = g;
           }
         double K[GD][GD];
-#if FA_ABL == 5
-#pragma unroll
-        for (int i = 0; i < GD; ++i)
-#pragma unroll
-          for (int jj = 0; jj < GD; ++jj) K[i][jj] = r[i * GD + jj] * lam + Ah[0] * mu;
-#else
         lin_block<GD>(G, lam, mu, K);
-#endif
-#if FA_ABL == 1
-        int s = lds_find(cols, lo, hi, cn[bb]);
-#elif FA_ABL == 2
-        int s = lo + (int)((uint32_t)cn[bb] % (uint32_t)(hi - lo));
-#else
-        int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_slot(cols, lo, hi, cn[bb], niter);
-#endif
+        int s = sl[0];  // rolled loop: shift the slot list instead of indexing it
+#pragma unroll
+        for (int k = 0; k + 1 < NBG; ++k) sl[k] = sl[k + 1];
         bad |= s < 0;
         s = s < 0 ? MAXB : s;
 #if FA_ABL == 3
@@ -1379,8 +1462,9 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
 #pragma unroll
           for (int jj = 0; jj < GD; ++jj) abl_sink += K[i][jj] * (double)s;
 #else
-        lds_add_block<GD>(acc, s, K, (mask >> (aloc * GD)) & ((1u << GD) - 1), (mask >> (b * GD)) & ((1u << GD) - 1));
+        lds_add_block<GD>(acc, s, K, rowm, (mask >> (b * GD)) & ((1u << GD) - 1));
 #endif
+        Ah += BS2;
       }
     } else {
       // non-affine tensor cells: J^-1 per quadrature point, read from the record as the rolled
@@ -1440,25 +1524,81 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
         lds_add_block<GD>(acc, s, K, (mask >> (aloc * GD)) & ((1u << GD) - 1), (mask >> (b * GD)) & ((1u << GD) - 1));
       }
     }
+  };
+  {
+    int it0 = tid;
+    if (IPF && have_pf) {
+      if (it0 < nitems) item(it0, std::true_type{});
+      it0 += 256;
+    }
+#if FA_ABL != 6
+    for (; it0 < nitems; it0 += 256) item(it0, std::false_type{});
+#endif
   }
 #if FA_ABL == 3
   if (abl_sink == 1.2345) acc[0] = abl_sink;
 #endif
+  have_pf = false;
+  if (IPF && nchunk < P.nchunks) {
+    have_pf = true;
+    const int na_n = (int)(nxt.a1 - nxt.a0);
+    if (tid < na_n * NSPLIT) {
+      const int64_t c = pflat_n / NN;
+      const int part = tid % NSPLIT;
+      const double2* rp = reinterpret_cast<const double2*>(P.rec + c * R::SIZE);
+#pragma unroll
+      for (int k = 0; k < RLP / 2; ++k) {
+        double2 v = rp[k];
+        pr[2 * k] = v.x;
+        pr[2 * k + 1] = v.y;
+      }
+#pragma unroll
+      for (int bb = 0; bb < NBG; ++bb) {
+        const int b = part * NBG + bb;
+        pcn[bb] = b < NN ? P.M.cells[c * NN + b] : -1;
+      }
+      pmask = P.bcmask ? P.bcmask[c] : 0u;
+    }
+  }
   if (bad) atomicOr(P.err, 1);
   __syncthreads();
-  if (P.bc) {
+  if (MAT == MAT_BLOCKS && P.bc) {
     for (int t = tid; t < nrows * GD; t += 256) {
       const int lr = t / GD, i = t % GD;
-      const int64_t r = r0 + lr;
-      if (!P.bc[r * GD + i]) continue;
-      const int s = lds_find(cols, rowoff[lr], rowoff[lr + 1], (int32_t)r);
+      if (!((s_rowbc[lr] >> i) & 1u)) continue;
+      const int s = lds_find(cols, rowoff[lr], rowoff[lr + 1], (int32_t)(r0 + lr));
       if (s < 0) { atomicOr(P.err, 2); continue; }
       acc[s * BS2 + i * GD + i] = P.diag;
     }
     __syncthreads();
   }
-  double* out = P.A.data + (b0 - P.A.indptr[P.A.row_begin]) * BS2;
-  for (int t = tid; t < nb * BS2; t += 256) out[t] = acc[t];
+  if (tid == 0) s_maxrow = 1;  // every lane has read it; the next stage max-reduces into it
+  // Stream the chunk out: 16-B non-temporal stores (the matrix is written once and not re-read
+  // by this launch, so it should not evict the records and dofmap the next chunks share).
+  {
+    const int64_t off = (b0 - P.A.indptr[P.A.row_begin]) * BS2;  // first value, in doubles
+    double* out = P.A.data + off;
+    const int nv = nb * BS2;
+    const int h = (int)(off & 1);  // one leading double when the chunk starts on an odd double
+#if FA_ABL == 8
+    if (acc[tid] == 1.2345e-300) out[tid] = 0.0;  // timing only: no chunk store
+    if (false) {
+#endif
+    if (h && tid == 0) __builtin_nontemporal_store(acc[0], out);
+    const int np = (nv - h) >> 1;
+    typedef double dv2 __attribute__((ext_vector_type(2)));
+    dv2* out2 = reinterpret_cast<dv2*>(out + h);
+    for (int t = tid; t < np; t += 256) {
+      dv2 v;
+      if (h) { v.x = acc[1 + 2 * t]; v.y = acc[2 + 2 * t]; }
+      else v = reinterpret_cast<const dv2*>(acc)[t];
+      __builtin_nontemporal_store(v, out2 + t);
+    }
+    if (((nv - h) & 1) && tid == 0) __builtin_nontemporal_store(acc[nv - 1], out + nv - 1);
+#if FA_ABL == 8
+    }
+#endif
+  }
   if (nchunk >= P.nchunks) break;
   __syncthreads();  // the store has read acc
   if (!PIPE) fetch(nxt);
@@ -1817,6 +1957,28 @@ static int chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
   return FA_OK;
 }
 
+// Gather grid. Default: one workgroup per chunk (capped below the 2^32 work-item limit; larger
+// plans loop, with chunk k+1's metadata in flight during chunk k). FEMASM_GATHER_GRID_MULT=m
+// launches a persistent grid of m x (CUs x occupancy) workgroups instead, each walking its
+// XCD's chunk range -- measured slower on config E (70.4 vs 64.5 ms at m = 1: the static chunk
+// assignment balances worse than the hardware dispatcher), kept as a measurement knob.
+template <typename K>
+static int64_t gather_grid(K kernel, int64_t nchunks) {
+  const int64_t per = (nchunks + 7) / 8;
+  const char* env = getenv("FEMASM_GATHER_GRID_MULT");
+  if (!env || atof(env) <= 0) return std::min<int64_t>(8 * per, kMaxBlocks);  // kMaxBlocks % 8 == 0
+  int dev = 0, cus = 256, occ = 4;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kernel, 256, 0) == hipSuccess && v > 0) occ = v;
+  }
+  const double mult = atof(env);
+  int64_t g = (int64_t)(cus * occ * mult);
+  g = std::max<int64_t>(8, g / 8 * 8);
+  return std::min<int64_t>(std::min<int64_t>(8 * per, g), kMaxBlocks);  // kMaxBlocks % 8 == 0
+}
+
 template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT>
 static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s) {
   using R = Rec<GD, NV, NQ, MAT>;
@@ -1836,8 +1998,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s) {
   if (P.nchunks > 0) {
     int64_t* desc = nullptr;
     if ((rc = chunk_desc(P, &desc, s))) return rc;
-    const int64_t per = (P.nchunks + 7) / 8;
-    const int64_t grid = std::min<int64_t>(8 * per, kMaxBlocks);  // kMaxBlocks % 8 == 0
+    const int64_t grid = gather_grid(k_gather<GD, NN, NV, NQ, NSPLIT, MAT>, P.nchunks);
     k_gather<GD, NN, NV, NQ, NSPLIT, MAT><<<(unsigned)grid, 256, 0, s>>>(P);
     LAUNCH_CHECK();
     HIP_TRY(hipFreeAsync(desc, s));
@@ -1873,8 +2034,7 @@ static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc,
   if (P.nchunks > 0) {
     int64_t* desc = nullptr;
     if ((rc = chunk_desc(P, &desc, s))) return rc;
-    const int64_t per = (P.nchunks + 7) / 8;
-    const int64_t grid = std::min<int64_t>(8 * per, kMaxBlocks);
+    const int64_t grid = gather_grid(k_gather<3, NN, 8, NQ, NSPLIT, MAT_BLOCKS>, P.nchunks);
     k_gather<3, NN, 8, NQ, NSPLIT, MAT_BLOCKS><<<(unsigned)grid, 256, 0, s>>>(P);
     LAUNCH_CHECK();
     HIP_TRY(hipFreeAsync(desc, s));

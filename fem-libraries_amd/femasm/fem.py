@@ -487,9 +487,10 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0):
         slots = None
         mode = os.environ.get("FEMASM_SLOTS", "auto")
         # Per (adjacency entry, column node) block position in its row: no LDS search in the
-        # kernel, for 2 B x nn^2 extra reads per cell. Measured (profiles/r1/slots.md): +21% on
-        # Q2 quads (long rows), +2% Q2 hex, -4% P2 tets (config E) -> default: tensor cells only.
-        if mode == "1" or (mode == "auto" and not is_simplex(V.mesh.cell_type)):
+        # kernel, for 2 B x nn^2 extra reads per cell. Measured with the interleaved-search
+        # kernel: config E 64.5 -> 61.0 ms, C 2.22 -> 2.15 ms, Q2 quads +21 % (profiles/r1/
+        # slots.md) -> on by default; FEMASM_SLOTS=0 keeps the in-kernel LDS search.
+        if mode in ("1", "auto"):
             slots = torch.empty(V.mesh.num_cells * V.nn * V.nn, dtype=torch.int16, device=V.mesh.device)
             _lib.check(L.fa_plan_slots(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), slots.data_ptr(),
                                        ctypes.byref(plan), sh), "fa_plan_slots")
