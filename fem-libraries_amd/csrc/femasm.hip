@@ -1979,23 +1979,43 @@ static int64_t gather_grid(K kernel, int64_t nchunks) {
   return std::min<int64_t>(std::min<int64_t>(8 * per, g), kMaxBlocks);  // kMaxBlocks % 8 == 0
 }
 
+// What a gather launch does: both stages with stream-ordered scratch (fa_assemble_matrix), or
+// one stage on a caller-owned work buffer (fa_gather_prepare / fa_gather_rows), or only report
+// that buffer's size.
+struct GatherStage {
+  enum { FULL, SIZE, PREP, ROWS } mode = FULL;
+  void* work = nullptr;
+  int64_t* bytes = nullptr;
+};
+static inline int64_t align256(int64_t b) { return (b + 255) & ~int64_t(255); }
+
 template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT>
-static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s) {
+static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const GatherStage& W) {
   using R = Rec<GD, NV, NQ, MAT>;
   static_assert(NN * GD <= 32, "bc mask holds 32 dofs");
   const int64_t nc = P.M.ncells;
+  const int64_t rec_bytes = align256((int64_t)sizeof(double) * R::SIZE * nc);
+  if (W.mode == GatherStage::SIZE) {
+    *W.bytes = rec_bytes + align256((int64_t)sizeof(uint32_t) * nc);
+    return FA_OK;
+  }
   double* rec = nullptr;
   uint32_t* mask = nullptr;
   int rc;
-  if ((rc = scratch_alloc((void**)&rec, sizeof(double) * R::SIZE * nc, s))) return rc;
-  if (bc && (rc = scratch_alloc((void**)&mask, sizeof(uint32_t) * nc, s))) return rc;
-  if (nc > 0) {
+  if (W.mode == GatherStage::FULL) {
+    if ((rc = scratch_alloc((void**)&rec, sizeof(double) * R::SIZE * nc, s))) return rc;
+    if (bc && (rc = scratch_alloc((void**)&mask, sizeof(uint32_t) * nc, s))) return rc;
+  } else {
+    rec = reinterpret_cast<double*>(W.work);
+    mask = bc ? reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.work) + rec_bytes) : nullptr;
+  }
+  if (nc > 0 && W.mode != GatherStage::ROWS) {
     k_cell_records<GD, NN, NV, NQ, MAT><<<grid_for(nc), 256, 0, s>>>(P.M, P.F, P.tab, bc, rec, mask);
     LAUNCH_CHECK();
   }
   P.rec = rec;
   P.bcmask = mask;
-  if (P.nchunks > 0) {
+  if (P.nchunks > 0 && W.mode != GatherStage::PREP) {
     int64_t* desc = nullptr;
     if ((rc = chunk_desc(P, &desc, s))) return rc;
     const int64_t grid = gather_grid(k_gather<GD, NN, NV, NQ, NSPLIT, MAT>, P.nchunks);
@@ -2003,8 +2023,10 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s) {
     LAUNCH_CHECK();
     HIP_TRY(hipFreeAsync(desc, s));
   }
-  HIP_TRY(hipFreeAsync(rec, s));
-  if (mask) HIP_TRY(hipFreeAsync(mask, s));
+  if (W.mode == GatherStage::FULL) {
+    HIP_TRY(hipFreeAsync(rec, s));
+    if (mask) HIP_TRY(hipFreeAsync(mask, s));
+  }
   return FA_OK;
 }
 
@@ -2017,12 +2039,20 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s) {
 // Hexahedra: MFMA element blocks into a stream-ordered block store, then the row gather sums
 // them (the "store pass + per-destination sum pass" alternative to global atomics).
 template <int NN, int NQ, int NSPLIT>
-static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc, hipStream_t s) {
+static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc, hipStream_t s, const GatherStage& W) {
   const int64_t nc = P.M.ncells;
+  if (W.mode == GatherStage::SIZE) {
+    *W.bytes = align256((int64_t)sizeof(double) * 9 * NN * NN * nc);
+    return FA_OK;
+  }
   double* eb = nullptr;
   int rc;
-  if ((rc = scratch_alloc((void**)&eb, sizeof(double) * 9 * NN * NN * nc, s))) return rc;
-  if (nc > 0) {
+  if (W.mode == GatherStage::FULL) {
+    if ((rc = scratch_alloc((void**)&eb, sizeof(double) * 9 * NN * NN * nc, s))) return rc;
+  } else {
+    eb = reinterpret_cast<double*>(W.work);
+  }
+  if (nc > 0 && W.mode != GatherStage::ROWS) {
     constexpr int thr = 64 * ((NN + 15) / 16) * ((NN + 15) / 16);
     const int grid = (int)std::min<int64_t>(nc, kMaxBlocks);
     BsrView none{nullptr, nullptr, nullptr, 0, 0};
@@ -2031,7 +2061,7 @@ static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc,
   }
   P.rec = eb;
   P.bcmask = nullptr;
-  if (P.nchunks > 0) {
+  if (P.nchunks > 0 && W.mode != GatherStage::PREP) {
     int64_t* desc = nullptr;
     if ((rc = chunk_desc(P, &desc, s))) return rc;
     const int64_t grid = gather_grid(k_gather<3, NN, 8, NQ, NSPLIT, MAT_BLOCKS>, P.nchunks);
@@ -2039,34 +2069,34 @@ static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc,
     LAUNCH_CHECK();
     HIP_TRY(hipFreeAsync(desc, s));
   }
-  HIP_TRY(hipFreeAsync(eb, s));
+  if (W.mode == GatherStage::FULL) HIP_TRY(hipFreeAsync(eb, s));
   return FA_OK;
 }
 
 static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const GatherArgs& P, const int8_t* bc,
-                           hipStream_t s, bool* handled) {
+                           hipStream_t s, bool* handled, const GatherStage& W = GatherStage()) {
   *handled = true;
   if (m->cell_type == FA_HEXAHEDRON && kind == FA_LINEAR_ELASTICITY) {
-    if (m->degree == 1 && T.nq == 8) return launch_hex_gather<8, 8, 1>(P, T, bc, s);
-    if (m->degree == 2 && T.nq == 27) return launch_hex_gather<27, 27, 3>(P, T, bc, s);
-    if (m->degree == 3 && T.nq == 64) return launch_hex_gather<64, 64, 8>(P, T, bc, s);
+    if (m->degree == 1 && T.nq == 8) return launch_hex_gather<8, 8, 1>(P, T, bc, s, W);
+    if (m->degree == 2 && T.nq == 27) return launch_hex_gather<27, 27, 3>(P, T, bc, s, W);
+    if (m->degree == 3 && T.nq == 64) return launch_hex_gather<64, 64, 8>(P, T, bc, s, W);
   }
   const int ct = m->cell_type, p = m->degree, nq = T.nq;
-  if (kind == FA_ASYM_DAMAGE) return launch_gather<2, 3, 3, 1, 1, FA_ASYM_DAMAGE>(P, bc, s);
+  if (kind == FA_ASYM_DAMAGE) return launch_gather<2, 3, 3, 1, 1, FA_ASYM_DAMAGE>(P, bc, s, W);
   if (kind == FA_NEO_HOOKEAN) {
-    if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, FA_NEO_NSPLIT, FA_NEO_HOOKEAN>(P, bc, s);
-    if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, FA_NEO_HOOKEAN>(P, bc, s);
-    if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, FA_NEO_HOOKEAN>(P, bc, s);
-    if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, FA_NEO_HOOKEAN>(P, bc, s);
+    if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, FA_NEO_NSPLIT, FA_NEO_HOOKEAN>(P, bc, s, W);
+    if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, FA_NEO_HOOKEAN>(P, bc, s, W);
+    if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, FA_NEO_HOOKEAN>(P, bc, s, W);
+    if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, FA_NEO_HOOKEAN>(P, bc, s, W);
     *handled = false;
     return FA_OK;
   }
-  if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, 0>(P, bc, s);
-  if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, 0>(P, bc, s);
-  if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, 0>(P, bc, s);
-  if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, FA_P2TET_NSPLIT, 0>(P, bc, s);
-  if (ct == FA_QUADRILATERAL && p == 1 && nq == 4) return launch_gather<2, 4, 4, 4, 1, 0>(P, bc, s);
-  if (ct == FA_QUADRILATERAL && p == 2 && nq == 9) return launch_gather<2, 9, 4, 9, 3, 0>(P, bc, s);
+  if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, 0>(P, bc, s, W);
+  if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, 0>(P, bc, s, W);
+  if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, 0>(P, bc, s, W);
+  if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, FA_P2TET_NSPLIT, 0>(P, bc, s, W);
+  if (ct == FA_QUADRILATERAL && p == 1 && nq == 4) return launch_gather<2, 4, 4, 4, 1, 0>(P, bc, s, W);
+  if (ct == FA_QUADRILATERAL && p == 2 && nq == 9) return launch_gather<2, 9, 4, 9, 3, 0>(P, bc, s, W);
   *handled = false;
   return FA_OK;
 }
@@ -2179,6 +2209,74 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     }
   }
   return FA_OK;
+}
+
+// ------------------------------------------------------------------------------------ split gather
+// fa_assemble_matrix(FA_GATHER) in two calls on a caller-owned work buffer, so that a caller can
+// assemble some rows (a rank's interface planes), start their exchange, and assemble the rest
+// while it runs -- without recomputing the per-cell records (femasm.parallel).
+static int gather_stage(const fa_mesh* mesh, const fa_form* form, const fa_adjacency* adj, const fa_plan* plan,
+                        const int8_t* bc, double diag, const fa_bsr* A, const GatherStage& W, hipStream_t s) {
+  int rc = check_mesh(mesh);
+  if (rc) return rc;
+  FormView F;
+  if ((rc = form_view(mesh, form, F))) return rc;
+  DevTables T;
+  if ((rc = get_tables(mesh->cell_type, mesh->degree, form->qdeg, &T))) return rc;
+  MeshView M{mesh->cells, mesh->geom, mesh->x, mesh->ncells, mesh->nnodes, mesh->nn, mesh->nv, mesh->gdim};
+  GatherArgs P{};
+  P.M = M; P.F = F;
+  P.A = BsrView{nullptr, nullptr, nullptr, 0, 0};
+  P.tab = T.wq; P.ahat = T.ahat; P.bc = bc; P.diag = diag;
+  static int* derr = nullptr;  // device error word of the split path
+  if (!derr) {
+    HIP_TRY(hipMalloc((void**)&derr, sizeof(int)));
+    HIP_TRY(hipMemset(derr, 0, sizeof(int)));
+  }
+  P.err = derr;
+  if (W.mode == GatherStage::ROWS) {
+    if (!A || !A->indptr || !A->indices || !A->data) return fail(FA_E_ARG, "null matrix");
+    if (A->bs != mesh->gdim || A->nrows != mesh->nnodes) return fail(FA_E_ARG, "matrix shape does not match mesh");
+    int64_t wb = A->row_begin, we = A->row_end;
+    if (we <= wb) { wb = 0; we = mesh->nnodes; }
+    if (wb < 0 || we > mesh->nnodes) return fail(FA_E_ARG, "row window out of range");
+    if (!adj || !adj->ptr || !adj->idx || !plan || !plan->row_start)
+      return fail(FA_E_ARG, "fa_gather_rows needs the adjacency and a plan (fa_plan_gather)");
+    P.A = BsrView{A->indptr, A->indices, A->data, wb, we};
+    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks;
+    P.slots = plan->slots;
+  }
+  bool handled = false;
+  rc = dispatch_gather(mesh, T, F.kind, P, bc, s, &handled, W);
+  if (rc) return rc;
+  if (!handled) return fail(FA_E_UNSUPPORTED, "no gather kernel for this element/form: use fa_assemble_matrix");
+  return FA_OK;
+}
+
+extern "C" int fa_gather_work_bytes(const fa_mesh* mesh, const fa_form* form, int64_t* bytes) {
+  if (!bytes) return fail(FA_E_ARG, "null bytes");
+  GatherStage W;
+  W.mode = GatherStage::SIZE;
+  W.bytes = bytes;
+  return gather_stage(mesh, form, nullptr, nullptr, nullptr, 0.0, nullptr, W, nullptr);
+}
+
+extern "C" int fa_gather_prepare(const fa_mesh* mesh, const fa_form* form, const int8_t* bc, void* work,
+                                 void* stream) {
+  if (!work) return fail(FA_E_ARG, "null work buffer");
+  GatherStage W;
+  W.mode = GatherStage::PREP;
+  W.work = work;
+  return gather_stage(mesh, form, nullptr, nullptr, bc, 0.0, nullptr, W, (hipStream_t)stream);
+}
+
+extern "C" int fa_gather_rows(const fa_mesh* mesh, const fa_form* form, const fa_adjacency* adj, const fa_plan* plan,
+                              const int8_t* bc, double diag, const void* work, fa_bsr* A, void* stream) {
+  if (!work) return fail(FA_E_ARG, "null work buffer");
+  GatherStage W;
+  W.mode = GatherStage::ROWS;
+  W.work = const_cast<void*>(work);
+  return gather_stage(mesh, form, adj, plan, bc, diag, A, W, (hipStream_t)stream);
 }
 
 // ------------------------------------------------------------------------------------ vectors (next rows)

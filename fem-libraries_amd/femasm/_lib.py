@@ -95,6 +95,9 @@ SIGNATURES = {
     "fa_plan_slots": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_tabulate_cells": (ctypes.c_int, [P, P, I64, I64, P, P]),
     "fa_assemble_matrix": (ctypes.c_int, [P, P, P, P, P, D, P, I32, P]),
+    "fa_gather_work_bytes": (ctypes.c_int, [P, P, P]),
+    "fa_gather_prepare": (ctypes.c_int, [P, P, P, P, P]),
+    "fa_gather_rows": (ctypes.c_int, [P, P, P, P, P, D, P, P, P]),
     "fa_assemble_vector": (ctypes.c_int, [P, P, P, P, P]),
     "fa_apply_lifting": (ctypes.c_int, [P, P, P, P, P, P, P, D, P]),
     "fa_set_bc": (ctypes.c_int, [P, I64, P, P, P, D, P]),

@@ -530,6 +530,62 @@ def assemble_matrix(a, bcs=None, diagonal: float = 1.0, A: MatrixCSR | None = No
     return A
 
 
+class SplitGather:
+    """fa_assemble_matrix(FA_GATHER) split into ``prepare()`` (per-cell records of all cells, once)
+    and ``rows(i)`` (the rows of ``ranges[i]`` of one row part of A), via fa_gather_prepare /
+    fa_gather_rows on a work buffer it owns. Each range is its own gather plan; every row of the
+    part must be in exactly one range for a complete assembly. femasm.parallel uses it to start
+    the interface exchange of a rank's slab while its interior rows assemble."""
+
+    def __init__(self, a, bcs, A: MatrixCSR, ranges, part: int = 0, diagonal: float = 1.0):
+        V = a.V
+        L = _lib.load()
+        self.L, self.a, self.A, self.diagonal = L, a, A, float(diagonal)
+        self.marker, _ = _combine_bcs(V, bcs)
+        self.fm, self.ff, self.adj = V._fa_mesh(), _fa_form(a), V._fa_adjacency()
+        dev = V.mesh.device
+        self.sh = _lib.stream_handle(dev)
+        nbytes = ctypes.c_int64(0)
+        _lib.check(L.fa_gather_work_bytes(ctypes.byref(self.fm), ctypes.byref(self.ff), ctypes.byref(nbytes)),
+                   "fa_gather_work_bytes")
+        self.work = torch.empty(max(int(nbytes.value), 16), dtype=torch.uint8, device=dev)
+        pr0, pr1, data = A.parts[part]
+        base = int(A.indptr[pr0])
+        bs2 = A.bs * A.bs
+        self.slots = None
+        if os.environ.get("FEMASM_SLOTS", "auto") in ("1", "auto"):
+            self.slots = torch.empty(V.mesh.num_cells * V.nn * V.nn, dtype=torch.int16, device=dev)
+        self.subs, self.plans, self._keep = [], [], []
+        for r0, r1 in ranges:
+            if not (pr0 <= r0 <= r1 <= pr1):
+                raise ValueError(f"row range [{r0}, {r1}) outside part [{pr0}, {pr1})")
+            fb = _fa_bsr(A, part)
+            fb.row_begin, fb.row_end = r0, r1
+            fb.data = data.data_ptr() + 8 * bs2 * (int(A.indptr[r0]) - base)
+            rs = torch.empty(r1 - r0 + 1, dtype=torch.int64, device=dev)
+            plan = _lib.fa_plan()
+            if r1 > r0:
+                _lib.check(L.fa_plan_gather(ctypes.byref(self.fm), ctypes.byref(self.adj), ctypes.byref(fb),
+                                            rs.data_ptr(), ctypes.byref(plan), self.sh), "fa_plan_gather")
+                if self.slots is not None:
+                    _lib.check(L.fa_plan_slots(ctypes.byref(self.fm), ctypes.byref(self.adj), ctypes.byref(fb),
+                                               self.slots.data_ptr(), ctypes.byref(plan), self.sh), "fa_plan_slots")
+            self.subs.append(fb)
+            self.plans.append(plan)
+            self._keep.append(rs)
+
+    def prepare(self):
+        _lib.check(self.L.fa_gather_prepare(ctypes.byref(self.fm), ctypes.byref(self.ff), _lib.ptr(self.marker),
+                                            self.work.data_ptr(), self.sh), "fa_gather_prepare")
+
+    def rows(self, i: int):
+        if self.plans[i].nchunks == 0:
+            return
+        _lib.check(self.L.fa_gather_rows(ctypes.byref(self.fm), ctypes.byref(self.ff), ctypes.byref(self.adj),
+                                         ctypes.byref(self.plans[i]), _lib.ptr(self.marker), self.diagonal,
+                                         self.work.data_ptr(), ctypes.byref(self.subs[i]), self.sh), "fa_gather_rows")
+
+
 def tabulate_cells(a, c0: int = 0, ncells: int | None = None) -> torch.Tensor:
     """Element matrices [nc, nn*bs, nn*bs] (batched ffcx tabulate_tensor / AssembleElementGrad)."""
     V = a.V

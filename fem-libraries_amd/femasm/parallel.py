@@ -112,9 +112,13 @@ def bc_diagonal_fixups(part: SlabPartition, indptr: torch.Tensor, indices: torch
 
 
 def exchange_interfaces(part: SlabPartition, values: torch.Tensor, slices: dict, groups, fixups=None,
-                        diagonal: float = 1.0):
+                        diagonal: float = 1.0, async_op: bool = False):
     """Sum the interface-plane rows with the slab neighbours (2-rank all-reduces), then reset the
-    Dirichlet diagonals of interface rows. `values` = the window's [nblocks_window, bs, bs]."""
+    Dirichlet diagonals of interface rows. `values` = the window's [nblocks_window, bs, bs].
+
+    async_op: only issue the all-reduces (RCCL runs them on its own stream, after the work
+    already queued on the current stream) and return a handle for ``finish_exchange``; the
+    caller can queue the interior rows meanwhile."""
     import torch.distributed as dist
 
     flat = values.reshape(values.shape[0], -1)
@@ -124,9 +128,24 @@ def exchange_interfaces(part: SlabPartition, values: torch.Tensor, slices: dict,
     if part.upper is not None:
         steps.append((part.rank, slices["upper"]))  # boundary q = rank
     # phase order: even boundaries first, then odd — consistent on both sides of every boundary
+    works = []
     for q, (b0, b1) in sorted(steps, key=lambda s: (s[0] % 2, s[0])):
         slab = flat[b0:b1]
-        dist.all_reduce(slab, op=dist.ReduceOp.SUM, group=groups[q])
+        works.append(dist.all_reduce(slab, op=dist.ReduceOp.SUM, group=groups[q], async_op=async_op))
+    handle = (works, values, fixups, diagonal)
+    if async_op:
+        return handle
+    finish_exchange(([], values, fixups, diagonal))
+    return None
+
+
+def finish_exchange(handle):
+    """Wait for the all-reduces of ``exchange_interfaces(async_op=True)`` (the current stream waits
+    on RCCL's) and reset the Dirichlet diagonals of the interface rows."""
+    works, values, fixups, diagonal = handle
+    for w in works:
+        if w is not None:
+            w.wait()
     if fixups is not None:
         values.view(-1)[fixups] = diagonal
 
@@ -169,15 +188,31 @@ class SlabProblem:
         self.bcs = [fem.dirichletbc(0.0, left, V), fem.dirichletbc([0.01, 0.0, 0.0], right, V)]
         marker, _ = fem._combine_bcs(V, self.bcs)
         self.V = V
-        fem.gather_plan(V, self.A, 0)
+        # rows in three kinds of range: the interface planes (assembled first, then exchanged
+        # while the interior rows assemble) and the interior
+        iface = [rr for rr in (part.lower, part.upper) if rr is not None]
+        inner = (part.row_begin + (part.plane if part.lower else 0), part.row_end - (part.plane if part.upper else 0))
+        self.split = fem.SplitGather(self.a, self.bcs, self.A, iface + [inner])
+        self.n_iface = len(iface)
         self.slices = interface_slices(part, self.A.indptr)
         self.fixups = bc_diagonal_fixups(part, self.A.indptr, self.A.indices, marker, 3)
         self.groups = groups if groups is not None else make_pair_groups(world)
         self.num_cells = m_asm.num_cells
-        self.kernel_name = "k_cell_records + k_gather<3,10,4,4,2,0> + 2-rank all_reduce(SUM) per slab boundary"
+        self.kernel_name = ("k_cell_records + k_gather<3,10,4,4,2,0> (interface planes, then interior rows) "
+                            "+ 2-rank all_reduce(SUM) per slab boundary overlapping the interior rows")
 
-    def assemble(self):
-        from . import fem
-
-        fem.assemble_matrix(self.a, bcs=self.bcs, A=self.A)
-        exchange_interfaces(self.part, self.A.parts[0][2], self.slices, self.groups, self.fixups)
+    def assemble(self, overlap: bool = True):
+        """Records of all cells; the interface-plane rows; their 2-rank all-reduces issued on
+        RCCL's stream; the interior rows on the compute stream meanwhile; wait; bc diagonals."""
+        sg = self.split
+        sg.prepare()
+        for i in range(self.n_iface):
+            sg.rows(i)
+        if overlap:
+            h = exchange_interfaces(self.part, self.A.parts[0][2], self.slices, self.groups, self.fixups,
+                                    async_op=True)
+            sg.rows(self.n_iface)
+            finish_exchange(h)
+        else:
+            sg.rows(self.n_iface)
+            exchange_interfaces(self.part, self.A.parts[0][2], self.slices, self.groups, self.fixups)

@@ -154,6 +154,19 @@ int fa_tabulate_cells(const fa_mesh* mesh, const fa_form* form, int64_t c0, int6
 int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, const fa_adjacency* adj, const fa_plan* plan,
                        const int8_t* bc, double diag, fa_bsr* A, int32_t flags, void* stream);
 
+/* Split gather: fa_assemble_matrix(FA_GATHER) as two calls sharing a caller-owned work buffer
+ * of fa_gather_work_bytes() bytes. fa_gather_prepare computes the per-cell records (geometry,
+ * material, tangent, constrained-dof masks) for ALL cells; fa_gather_rows then assembles the
+ * rows of `plan` (any sub-window of A: several plans over disjoint row ranges may be run in any
+ * order, e.g. a rank's interface planes first, their exchange overlapping the interior rows).
+ * `bc` must be the same in both calls. Same semantics per row as fa_assemble_matrix; elements /
+ * forms without a gather kernel return FA_E_UNSUPPORTED. (Replaces the same dolfinx call,
+ * FEniCSx/mechanic2d/asym_elasto_damage_model.cc:852-857, as fa_assemble_matrix.) */
+int fa_gather_work_bytes(const fa_mesh* mesh, const fa_form* form, int64_t* bytes);
+int fa_gather_prepare(const fa_mesh* mesh, const fa_form* form, const int8_t* bc, void* work, void* stream);
+int fa_gather_rows(const fa_mesh* mesh, const fa_form* form, const fa_adjacency* adj, const fa_plan* plan,
+                   const int8_t* bc, double diag, const void* work, fa_bsr* A, void* stream);
+
 /* Residual b += int sigma(u):eps(v) dx_q - int f.v dx_{2p} (b is ADDED into, like dolfinx
  * assemble_vector; the reference zeroes it first). sigma term on the form's quadrature degree
  * (the reference's `dxx`), load term on degree 2p (the reference's default `dx`). Node-parallel

@@ -27,7 +27,7 @@ def _bc_marker(xs, bs):
     return on.repeat_interleave(bs).to(torch.int8)
 
 
-def _worker(rank, world, port, n):
+def _worker(rank, world, port, n, async_op=False):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -60,7 +60,11 @@ def _worker(rank, world, port, n):
     slices = parallel.interface_slices(part, ip_t)
     fix = parallel.bc_diagonal_fixups(part, ip_t, ix_t, marker, bs)
     groups = parallel.make_pair_groups(world)
-    parallel.exchange_interfaces(part, window, slices, groups, fix)
+    if async_op:  # the overlapped form SlabProblem.assemble uses: issue, (interior work), finish
+        h = parallel.exchange_interfaces(part, window, slices, groups, fix, async_op=True)
+        parallel.finish_exchange(h)
+    else:
+        parallel.exchange_interfaces(part, window, slices, groups, fix)
 
     # global reference
     m = mesh.create_unit_cube(n, n, n, ct)
@@ -83,9 +87,9 @@ def _worker(rank, world, port, n):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 4), (3, 5), (4, 4)])
-def test_slab_exchange_gloo(world, n):
-    mp.spawn(_worker, args=(world, _free_port(), n), nprocs=world, join=True)
+@pytest.mark.parametrize("world,n,async_op", [(2, 4, False), (3, 5, False), (4, 4, False), (3, 5, True), (4, 4, True)])
+def test_slab_exchange_gloo(world, n, async_op):
+    mp.spawn(_worker, args=(world, _free_port(), n, async_op), nprocs=world, join=True)
 
 
 def test_slab_partition_covers_all_layers():

@@ -10,10 +10,11 @@ passes=(
   "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"
   "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU"
   "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS"
+  "SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_FLAT"
 )
 i=0
 for p in "${passes[@]}"; do
-  timeout -k 10 600 rocprofv3 --kernel-include-regex "$kre" --pmc $p -d "$out/pass$i" -o run --output-format csv -- "$@" > "$out/pass$i.log" 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
+  timeout -s KILL 300 rocprofv3 --kernel-include-regex "$kre" --pmc $p -d "$out/pass$i" -o run --output-format csv -- "$@" > "$out/pass$i.log" 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
   i=$((i+1))
 done
 echo "passes ok"
