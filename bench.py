@@ -143,23 +143,31 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="E", choices=sorted(CONFIGS))
-    ap.add_argument("--n", type=int, default=None, help="cells per side (default: the config's)")
+    ap.add_argument("--side", "--n", dest="n", type=int, default=None,
+                    help="cells per side (default: the config's); use --side under torchrun")
     ap.add_argument("--method", default="gather", choices=["gather", "scatter"])
     ap.add_argument("--cpu-sample-n", type=int, default=24)
     ap.add_argument("--cpu-reps", type=int, default=7)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true", help="N > 1: exchange after all rows (no overlap)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local_rank)
+    # one GPU per rank; FEMASM_DIST_BACKEND=gloo rehearses N > 1 with ranks sharing the visible GPUs
+    backend = os.environ.get("FEMASM_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local_rank % max(ndev, 1) if backend == "gloo" else local_rank)
     torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        else:
+            dist.init_process_group(backend)
 
     from femasm import fem
 
@@ -170,8 +178,12 @@ def main():
     if world > 1:
         from femasm import parallel
 
+        if args.config != "E":
+            raise SystemExit("N > 1 shards config E's mesh (P2 tets, linear elasticity) only")
         prob = parallel.SlabProblem(n, rank, world, dev)
-        step = prob.assemble
+
+        def step():
+            prob.assemble(overlap=not args.no_overlap)
         ncells_local = prob.num_cells
         kernel_name = prob.kernel_name
     else:
