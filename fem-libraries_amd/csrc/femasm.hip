@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdlib>
+#include <cstring>
 #include <cstdio>
 #include <map>
 #include <mutex>
@@ -858,6 +859,7 @@ struct GatherArgs {
   const int64_t* chunk_b;  // [nchunks + 1] indptr[row_start[c]] (k_chunk_desc)
   const int64_t* chunk_a;  // [nchunks + 1] adj_ptr[row_start[c]]
   int64_t nchunks;
+  unsigned long long* ctr;  // [8] per-XCD chunk counters (dynamic persistent grid), or NULL
   const uint16_t* slots;  // optional [adjacency entry][NN] position of the block within its row
   const int8_t* bc;
   double diag;
@@ -1053,7 +1055,8 @@ __device__ __forceinline__ void lds_add_block(double* acc, int s, double (&K)[GD
 #define FA_GATHER_UNROLL_B 1
 #endif
 // Timing-only ablations of the affine-simplex gather (wrong results; tools/ablate.sh):
-// 3 no LDS adds, 6 no item loop (chunk setup + store only), 7 no per-item global loads,
+// 3 no LDS adds, 4 no reference-tensor LDS reads, 6 no item loop (chunk setup + store only),
+// 7 no per-item global loads,
 // 8 no chunk store, 9 no record loads (column ids and bc mask still loaded)
 #ifndef FA_ABL
 #define FA_ABL 0
@@ -1102,8 +1105,42 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     const int64_t c = (v % 8) * per + v / 8;
     return c < P.nchunks ? c : P.nchunks;
   };
+  // Chunk sequence of this workgroup. Static (P.ctr == NULL): chunk_of(blockIdx.x + k*gridDim.x).
+  // Dynamic (persistent grid): lane 0 takes the next chunk of its XCD's range from a per-XCD
+  // counter (blockIdx.x % 8 = the XCD under round-robin dispatch; exhausted ranges are left for
+  // the next one), three chunks ahead so the atomic's latency hides behind a chunk's work; the
+  // index reaches the other lanes through LDS.
+  __shared__ int64_t s_idx[3];
+  uint32_t qdone = 0u;  // lane 0: ranges found exhausted
+  auto grab = [&]() -> int64_t {
+    for (int t = 0; t < 8; ++t) {
+      const int q = (int)((blockIdx.x + t) & 7);
+      if ((qdone >> q) & 1u) continue;
+      const unsigned long long c = atomicAdd(P.ctr + q, 1ull);
+      const int64_t ch = q * per + (int64_t)c;
+      if ((int64_t)c < per && ch < P.nchunks) return ch;
+      qdone |= 1u << q;
+    }
+    return P.nchunks;
+  };
   int64_t vb = blockIdx.x;
-  if (chunk_of(vb) >= P.nchunks) return;  // whole workgroup idle
+  int64_t idx0, idx1, idx2;
+  if (P.ctr) {
+    if (tid == 0) {
+      s_idx[0] = grab();
+      s_idx[1] = grab();
+      s_idx[2] = grab();
+    }
+    __syncthreads();
+    idx0 = s_idx[0];
+    idx1 = s_idx[1];
+    idx2 = s_idx[2];
+  } else {
+    idx0 = chunk_of(vb);
+    idx1 = chunk_of(vb + vstep);
+    idx2 = chunk_of(vb + 2 * vstep);
+  }
+  if (idx0 >= P.nchunks) return;  // whole workgroup idle
 
   if constexpr (MAT == MAT_BLOCKS) {
   } else if constexpr (NEO) {
@@ -1212,20 +1249,23 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   bool have_pf = false;
   if (tid == 0) s_maxrow = 1;
   __syncthreads();
-  Desc cur = load_desc(chunk_of(vb));
+  Desc cur = load_desc(idx0);
   fetch(cur);
   stage(cur);
-  int64_t nchunk = chunk_of(vb + vstep);
+  int64_t nchunk = idx1;   // chunk k+1 (its descriptor is loaded, its metadata staged next)
+  int64_t nnchunk = idx2;  // chunk k+2 (its descriptor is loaded during chunk k)
   Desc nxt = nchunk < P.nchunks ? load_desc(nchunk) : cur;
   __syncthreads();
+  int kpar = 0;
   for (;;) {
+  if (P.ctr && tid == 0) s_idx[kpar] = nnchunk < P.nchunks ? grab() : P.nchunks;  // chunk k+3
+
   if (PIPE && nchunk < P.nchunks) fetch(nxt);  // lands while this chunk is assembled
   if (IPF && nchunk < P.nchunks) {
     const int na_n = (int)(nxt.a1 - nxt.a0);
     if (tid < na_n * NSPLIT)
       pflat_n = P.adj_idx[nxt.a0 + perm(tid / NSPLIT, na_n, perm_stride(na_n), 1.0f / (float)na_n)];
   }
-  const int64_t nnchunk = chunk_of(vb + 2 * vstep);
   const Desc nn2 = nnchunk < P.nchunks ? load_desc(nnchunk) : nxt;
 
   const int64_t r0 = cur.r0;
@@ -1429,14 +1469,22 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       for (int bb = 0; bb < NBG; ++bb) {
         const int b = part * NBG + bb;
         if (NN % NSPLIT != 0 && b >= NN) break;
+#if FA_ABL == 4
+        double Ahr[BS2];
+#pragma unroll
+        for (int e = 0; e < BS2; ++e) Ahr[e] = 0.1 * (e + aloc) + bb;
+        const double* Ahp = Ahr;
+#else
+        const double* Ahp = Ah;
+#endif
         double T[GD][GD];  // T = Ahat Ji
 #pragma unroll
         for (int i = 0; i < GD; ++i)
 #pragma unroll
           for (int d = 0; d < GD; ++d) {
-            double t = Ah[i * GD] * r[d];
+            double t = Ahp[i * GD] * r[d];
 #pragma unroll
-            for (int k = 1; k < GD; ++k) t = fma(Ah[i * GD + k], r[k * GD + d], t);
+            for (int k = 1; k < GD; ++k) t = fma(Ahp[i * GD + k], r[k * GD + d], t);
             T[i][d] = t;
           }
         double G[GD][GD];  // G = Ji^T T
@@ -1606,6 +1654,8 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   cur = nxt;
   nxt = nn2;
   nchunk = nnchunk;
+  nnchunk = P.ctr ? s_idx[kpar] : chunk_of(vb + 3 * vstep);  // written before the items barrier
+  kpar ^= 1;
   vb += vstep;
   __syncthreads();
   }
@@ -1946,34 +1996,46 @@ __global__ void k_chunk_desc(const int64_t* __restrict__ row_start, int64_t nchu
   }
 }
 
+static bool gather_dynamic() {
+  const char* e = getenv("FEMASM_GATHER_SCHED");
+  return !(e && strcmp(e, "static") == 0);
+}
+
 static int chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
   int rc;
-  if ((rc = scratch_alloc((void**)buf, sizeof(int64_t) * 2 * (P.nchunks + 1), s))) return rc;
+  if ((rc = scratch_alloc((void**)buf, sizeof(int64_t) * (2 * (P.nchunks + 1) + 8), s))) return rc;
   P.chunk_b = *buf;
   P.chunk_a = *buf + (P.nchunks + 1);
+  P.ctr = nullptr;
+  if (gather_dynamic()) {
+    P.ctr = reinterpret_cast<unsigned long long*>(*buf + 2 * (P.nchunks + 1));
+    HIP_TRY(hipMemsetAsync(P.ctr, 0, 8 * sizeof(unsigned long long), s));
+  }
   k_chunk_desc<<<grid_for(P.nchunks + 1), 256, 0, s>>>(P.row_start, P.nchunks, P.A.indptr, P.adj_ptr, *buf,
                                                       *buf + (P.nchunks + 1));
   LAUNCH_CHECK();
   return FA_OK;
 }
 
-// Gather grid. Default: one workgroup per chunk (capped below the 2^32 work-item limit; larger
-// plans loop, with chunk k+1's metadata in flight during chunk k). FEMASM_GATHER_GRID_MULT=m
-// launches a persistent grid of m x (CUs x occupancy) workgroups instead, each walking its
-// XCD's chunk range -- measured slower on config E (70.4 vs 64.5 ms at m = 1: the static chunk
-// assignment balances worse than the hardware dispatcher), kept as a measurement knob.
+// Gather grid. Default (dynamic): a persistent grid of the resident workgroup count (CUs x
+// occupancy, a multiple of 8 for the XCD order), each workgroup pulling chunks from its XCD's
+// counter with three chunks of look-ahead, so chunk k's stores, chunk k+1's metadata loads and
+// the per-workgroup LDS tables overlap the work instead of heading every chunk (measured on
+// config E: skeleton 41.9 -> 33.0 ms persistent). FEMASM_GATHER_SCHED=static: one workgroup per
+// chunk (capped below the 2^32 work-item limit; larger plans loop). FEMASM_GATHER_GRID_MULT=m
+// scales the persistent grid (measurement knob).
 template <typename K>
 static int64_t gather_grid(K kernel, int64_t nchunks) {
   const int64_t per = (nchunks + 7) / 8;
   const char* env = getenv("FEMASM_GATHER_GRID_MULT");
-  if (!env || atof(env) <= 0) return std::min<int64_t>(8 * per, kMaxBlocks);  // kMaxBlocks % 8 == 0
+  if (!gather_dynamic()) return std::min<int64_t>(8 * per, kMaxBlocks);  // kMaxBlocks % 8 == 0
   int dev = 0, cus = 256, occ = 4;
   if (hipGetDevice(&dev) == hipSuccess) {
     int v = 0;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kernel, 256, 0) == hipSuccess && v > 0) occ = v;
   }
-  const double mult = atof(env);
+  const double mult = (env && atof(env) > 0) ? atof(env) : 1.0;
   int64_t g = (int64_t)(cus * occ * mult);
   g = std::max<int64_t>(8, g / 8 * 8);
   return std::min<int64_t>(std::min<int64_t>(8 * per, g), kMaxBlocks);  // kMaxBlocks % 8 == 0
