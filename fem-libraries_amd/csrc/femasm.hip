@@ -969,6 +969,14 @@ __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, co
   }
 }
 
+// Workgroup-uniform load through the scalar cache: a constant-address-space pointer lets the
+// compiler emit s_load (counted by lgkmcnt) instead of a vector load, whose vmcnt wait would also
+// drain every earlier vector load AND store of the wave (CDNA counts stores in vmcnt).
+template <typename T>
+__device__ __forceinline__ T sload(const T* p, int64_t i) {
+  return ((const __attribute__((address_space(4))) T*)p)[i];
+}
+
 // binary search of `col` in cols[lo, hi) (LDS)
 __device__ __forceinline__ int lds_find(const int32_t* cols, int lo, int hi, int32_t col) {
   int l = lo, h = hi - 1;
@@ -1061,6 +1069,15 @@ __device__ __forceinline__ void lds_add_block(double* acc, int s, double (&K)[GD
 #ifndef FA_ABL
 #define FA_ABL 0
 #endif
+#ifndef FA_GATHER_TIMING
+#define FA_GATHER_TIMING 0  // 1: per-phase shader-clock totals of the gather (measurement build)
+#endif
+#if FA_GATHER_TIMING
+__device__ unsigned long long g_gather_timing[8];
+#define GT_MARK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define GT_MARK(v)
+#endif
 #ifndef FA_GATHER_CN_ALWAYS
 #define FA_GATHER_CN_ALWAYS 0
 #endif
@@ -1079,7 +1096,6 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   constexpr int NBG = (NN + NSPLIT - 1) / NSPLIT;  // column nodes per item
   __shared__ double acc[(MAXB + 1) * BS2];  // + one sink slot for (erroneous) missing columns
   __shared__ int32_t cols[MAXB];
-  __shared__ int s_maxrow;
   __shared__ int32_t rowoff[kGatherMaxRows + 1];
   __shared__ uint8_t s_rowbc[kGatherMaxRows];  // constrained-dof bits of each chunk row
   __shared__ uint8_t adjrow[kGatherMaxAdj];
@@ -1090,6 +1106,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   __shared__ double s_ahat[SIMP ? NN * NN * BS2 : 1];
 
   const int tid = threadIdx.x;
+  const int64_t abase = sload(P.A.indptr, P.A.row_begin);  // block index of the window's first value
   constexpr int NPC = (MAXB + 255) / 256;           // column indices per thread (metadata slice)
   constexpr int NPA = (kGatherMaxAdj + 255) / 256;  // adjacency entries per thread
   static_assert(kGatherMaxRows < 256, "one row offset per thread");
@@ -1132,9 +1149,9 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       s_idx[2] = grab();
     }
     __syncthreads();
-    idx0 = s_idx[0];
-    idx1 = s_idx[1];
-    idx2 = s_idx[2];
+    idx0 = __builtin_amdgcn_readfirstlane((int)s_idx[0]);  // nchunks < 2^31 (checked on the host)
+    idx1 = __builtin_amdgcn_readfirstlane((int)s_idx[1]);
+    idx2 = __builtin_amdgcn_readfirstlane((int)s_idx[2]);
   } else {
     idx0 = chunk_of(vb);
     idx1 = chunk_of(vb + vstep);
@@ -1158,47 +1175,54 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   // descriptor of chunk k+2 is loaded, so a chunk starts with one exposed latency (its cells'
   // records) instead of four dependent ones (measured: the un-pipelined skeleton alone took
   // 46 of 84 ms on config E, tools/ablate.sh FA_ABL=6).
-  struct Desc { int64_t r0, r1, b0, b1, a0, a1; };
+  // rows and adjacency entries fit 32 bits (the ABI checks ncells*nn < 2^31); block indices may not
+  struct Desc { int64_t b0, b1; int32_t r0, r1, a0, a1; };
   auto load_desc = [&](int64_t c) -> Desc {
-    return Desc{P.row_start[c], P.row_start[c + 1], P.chunk_b[c], P.chunk_b[c + 1], P.chunk_a[c], P.chunk_a[c + 1]};
+    return Desc{sload(P.chunk_b, c), sload(P.chunk_b, c + 1), (int32_t)sload(P.row_start, c),
+                (int32_t)sload(P.row_start, c + 1), (int32_t)sload(P.chunk_a, c), (int32_t)sload(P.chunk_a, c + 1)};
   };
   int32_t pc[NPC], pj[NPA];
   // row / adjacency pointers: low 32 bits only (differences within a chunk are < 2^31)
-  uint32_t prow = 0, prow1 = 0, pa0 = 0, pa1 = 0, pbc = 0;
+  uint32_t prow = 0, pa0 = 0, pa1 = 0;
+  uint32_t pbc[GD];  // raw constrained-dof bytes of row tid, combined in stage
   const uint32_t* indptr_lo = reinterpret_cast<const uint32_t*>(P.A.indptr);
   const uint32_t* adjptr_lo = reinterpret_cast<const uint32_t*>(P.adj_ptr);
+  // Loads at clamped indices, unconditionally and with no use of their values here: a
+  // per-load "load or constant" select makes hipcc branch around each load and wait for it,
+  // which serialises the prefetch; stage() ignores the lanes past the chunk's counts.
   auto fetch = [&](const Desc& d) {
     const int nb_ = (int)(d.b1 - d.b0), nr_ = (int)(d.r1 - d.r0), na_ = (int)(d.a1 - d.a0);
+    if (nb_ > 0) {
 #pragma unroll
-    for (int k = 0; k < NPC; ++k) {
-      const int t = tid + 256 * k;
-      pc[k] = t < nb_ ? P.A.indices[d.b0 + t] : 0;
+      for (int k = 0; k < NPC; ++k) pc[k] = P.A.indices[d.b0 + min(tid + 256 * k, nb_ - 1)];
     }
-    prow = tid <= nr_ ? indptr_lo[2 * (d.r0 + tid)] : 0u;
-    prow1 = tid < nr_ ? indptr_lo[2 * (d.r0 + tid + 1)] : prow;
-    pa0 = tid < nr_ ? adjptr_lo[2 * (d.r0 + tid)] : 0u;
-    pa1 = tid < nr_ ? adjptr_lo[2 * (d.r0 + tid + 1)] : 0u;
-    pbc = 0u;
-    if (P.bc && tid < nr_) {
+    const int rr = min(tid, nr_), rr1 = min(tid + 1, nr_);
+    prow = indptr_lo[2 * (d.r0 + rr)];
+    pa0 = adjptr_lo[2 * (d.r0 + rr)];
+    pa1 = adjptr_lo[2 * (d.r0 + rr1)];
+    if (P.bc && nr_ > 0) {
+      const uint8_t* bp = reinterpret_cast<const uint8_t*>(P.bc) + (d.r0 + min(tid, nr_ - 1)) * GD;
 #pragma unroll
-      for (int i = 0; i < GD; ++i) pbc |= (P.bc[(d.r0 + tid) * GD + i] ? 1u : 0u) << i;
+      for (int i = 0; i < GD; ++i) pbc[i] = bp[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < GD; ++i) pbc[i] = 0u;
     }
+    if (na_ > 0) {
 #pragma unroll
-    for (int k = 0; k < NPA; ++k) {
-      const int t = tid + 256 * k;
-      pj[k] = t < na_ ? P.adj_idx[d.a0 + t] : 0;
+      for (int k = 0; k < NPA; ++k) pj[k] = P.adj_idx[d.a0 + min(tid + 256 * k, na_ - 1)];
     }
   };
-  auto stage = [&](const Desc& d) {  // registers -> LDS, accumulator zeroed
+  // Metadata of a chunk: registers -> LDS. Runs right after the previous chunk's items barrier
+  // and BEFORE its store, so the wait for the prefetched registers does not also wait for the
+  // store's writes (vmcnt counts stores, and the store loop's trip count is not static).
+  auto stage_meta = [&](const Desc& d) {
     const int nb_ = (int)(d.b1 - d.b0), nr_ = (int)(d.r1 - d.r0), na_ = (int)(d.a1 - d.a0);
-    {
-      double2* acc2 = reinterpret_cast<double2*>(acc);
-      const int nv2 = (nb_ * BS2 + 1) >> 1;  // acc holds (MAXB + 1) blocks: the odd tail fits
-      for (int t = tid; t < nv2; t += 256) acc2[t] = make_double2(0.0, 0.0);
-    }
     if (tid < nr_) {
-      s_rowbc[tid] = (uint8_t)pbc;
-      atomicMax(&s_maxrow, (int)(prow1 - prow));  // s_maxrow was reset during the previous store
+      uint32_t bits = 0u;
+#pragma unroll
+      for (int i = 0; i < GD; ++i) bits |= (pbc[i] != 0u ? 1u : 0u) << i;
+      s_rowbc[tid] = (uint8_t)bits;
     }
 #pragma unroll
     for (int k = 0; k < NPC; ++k) {
@@ -1215,6 +1239,12 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       const int t = tid + 256 * k;
       if (t < na_) s_adj[t] = pj[k];
     }
+  };
+  auto zero_acc = [&](const Desc& d) {  // after the barrier that follows the previous store
+    const int nb_ = (int)(d.b1 - d.b0);
+    double2* acc2 = reinterpret_cast<double2*>(acc);
+    const int nv2 = (nb_ * BS2 + 1) >> 1;  // acc holds (MAXB + 1) blocks: the odd tail fits
+    for (int t = tid; t < nv2; t += 256) acc2[t] = make_double2(0.0, 0.0);
   };
 
   // neo-Hookean items hold large per-q tangents: the prefetch registers would spill there
@@ -1243,30 +1273,45 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   constexpr bool IPF = FA_GATHER_IPF && SIMP && !NEO && MAT != MAT_BLOCKS && FA_ABL == 0;
   constexpr int RLP = IPF ? R::SIZE : 2;
   double pr[RLP];
-  int32_t pcn[NBG];
+  int32_t pcn[NBG];  // column node ids (in-kernel search) or slot offsets (slot map)
   uint32_t pmask = 0u;
-  int32_t pflat_n = 0;
+  int32_t pflat_n = 0, pj_n = 0;
   bool have_pf = false;
-  if (tid == 0) s_maxrow = 1;
-  __syncthreads();
   Desc cur = load_desc(idx0);
   fetch(cur);
-  stage(cur);
+  stage_meta(cur);
+  zero_acc(cur);
   int64_t nchunk = idx1;   // chunk k+1 (its descriptor is loaded, its metadata staged next)
   int64_t nnchunk = idx2;  // chunk k+2 (its descriptor is loaded during chunk k)
   Desc nxt = nchunk < P.nchunks ? load_desc(nchunk) : cur;
   __syncthreads();
   int kpar = 0;
+#if FA_GATHER_TIMING
+  unsigned long long gt[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long gt_top = __builtin_amdgcn_s_memtime();
+#endif
   for (;;) {
-  if (P.ctr && tid == 0) s_idx[kpar] = nnchunk < P.nchunks ? grab() : P.nchunks;  // chunk k+3
+  // chunk k+3: lane 0 issues the counter atomic here and resolves it after the items, so the
+  // wait for its return (a vmcnt wait) does not head the chunk
+  unsigned long long gcand = 0ull;
+  int gq = -1;
+  if (P.ctr && tid == 0 && nnchunk < P.nchunks) {
+    for (int t = 0; t < 8; ++t) {
+      const int q = (int)((blockIdx.x + t) & 7);
+      if (!((qdone >> q) & 1u)) { gq = q; break; }
+    }
+    if (gq >= 0) gcand = atomicAdd(P.ctr + gq, 1ull);
+  }
 
   if (PIPE && nchunk < P.nchunks) fetch(nxt);  // lands while this chunk is assembled
   if (IPF && nchunk < P.nchunks) {
     const int na_n = (int)(nxt.a1 - nxt.a0);
-    if (tid < na_n * NSPLIT)
-      pflat_n = P.adj_idx[nxt.a0 + perm(tid / NSPLIT, na_n, perm_stride(na_n), 1.0f / (float)na_n)];
+    if (tid < na_n * NSPLIT) {
+      pj_n = perm(tid / NSPLIT, na_n, perm_stride(na_n), 1.0f / (float)na_n);
+      pflat_n = P.adj_idx[nxt.a0 + pj_n];
+    }
   }
-  const Desc nn2 = nnchunk < P.nchunks ? load_desc(nnchunk) : nxt;
+  Desc nn2;  // chunk k+2's descriptor: loaded after the items (scalar loads), used from the next chunk on
 
   const int64_t r0 = cur.r0;
   const int nrows = (int)(cur.r1 - cur.r0);
@@ -1274,7 +1319,9 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   const int nb = (int)(cur.b1 - cur.b0);
   const int64_t a0 = cur.a0;
   const int na = (int)(cur.a1 - cur.a0);
-  const int niter = 32 - __clz(s_maxrow);  // >= ceil(log2(maxrow)) + 0/1 halvings to reach n == 1
+  // fixed trip count of the in-kernel slot search: enough halvings for any row of a chunk
+  // (<= MAXB blocks); extra ones are no-ops once the interval has one entry
+  constexpr int niter = 32 - __builtin_clz((unsigned)MAXB);
   int bad = 0;
   // Dirichlet diagonals (dolfinx set_diagonal) before the items: no item adds into a constrained
   // dof's diagonal entry (its row bit masks the add), so this needs no barrier. The block-store
@@ -1456,7 +1503,10 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       // affine simplex: G_ab = |J| Ji^T Ahat_ab Ji  (reference-tensor form)
       const double wdet = r[BS2], lam = r[BS2 + 1] * wdet, mu = r[BS2 + 2] * wdet;
       int sl[NBG];  // slots of the item's column nodes, searched together
-      if (P.slots) {
+      if (decltype(FROMPF)::value && P.slots) {  // prefetched slot offsets
+#pragma unroll
+        for (int bb = 0; bb < NBG; ++bb) sl[bb] = lo + cn[bb];
+      } else if (P.slots) {
 #pragma unroll
         for (int bb = 0; bb < NBG; ++bb)
           sl[bb] = part * NBG + bb < NN ? lo + (int)P.slots[(a0 + j) * NN + part * NBG + bb] : 0;
@@ -1600,16 +1650,38 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
         pr[2 * k] = v.x;
         pr[2 * k + 1] = v.y;
       }
+      if (P.slots) {
 #pragma unroll
-      for (int bb = 0; bb < NBG; ++bb) {
-        const int b = part * NBG + bb;
-        pcn[bb] = b < NN ? P.M.cells[c * NN + b] : -1;
+        for (int bb = 0; bb < NBG; ++bb) {
+          const int b = part * NBG + bb;
+          pcn[bb] = b < NN ? (int32_t)P.slots[(nxt.a0 + pj_n) * NN + b] : 0;
+        }
+      } else {
+#pragma unroll
+        for (int bb = 0; bb < NBG; ++bb) {
+          const int b = part * NBG + bb;
+          pcn[bb] = b < NN ? P.M.cells[c * NN + b] : -1;
+        }
       }
       pmask = P.bcmask ? P.bcmask[c] : 0u;
     }
   }
+  nn2 = nnchunk < P.nchunks ? load_desc(nnchunk) : nxt;
+  if (P.ctr && tid == 0) {
+    int64_t ch = P.nchunks;
+    if (gq >= 0) {
+      ch = gq * per + (int64_t)gcand;
+      if (!((int64_t)gcand < per && ch < P.nchunks)) {
+        qdone |= 1u << gq;
+        ch = grab();
+      }
+    }
+    s_idx[kpar] = ch;
+  }
   if (bad) atomicOr(P.err, 1);
+  GT_MARK(gt_b);
   __syncthreads();
+  GT_MARK(gt_c);
   if (MAT == MAT_BLOCKS && P.bc) {
     for (int t = tid; t < nrows * GD; t += 256) {
       const int lr = t / GD, i = t % GD;
@@ -1620,11 +1692,14 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     }
     __syncthreads();
   }
-  if (tid == 0) s_maxrow = 1;  // every lane has read it; the next stage max-reduces into it
+  if (nchunk < P.nchunks) {  // chunk k+1's metadata: every lane is past chunk k's items
+    if (!PIPE) fetch(nxt);
+    stage_meta(nxt);
+  }
   // Stream the chunk out: 16-B non-temporal stores (the matrix is written once and not re-read
   // by this launch, so it should not evict the records and dofmap the next chunks share).
   {
-    const int64_t off = (b0 - P.A.indptr[P.A.row_begin]) * BS2;  // first value, in doubles
+    const int64_t off = (b0 - abase) * BS2;  // first value, in doubles
     double* out = P.A.data + off;
     const int nv = nb * BS2;
     const int h = (int)(off & 1);  // one leading double when the chunk starts on an odd double
@@ -1636,29 +1711,61 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     const int np = (nv - h) >> 1;
     typedef double dv2 __attribute__((ext_vector_type(2)));
     dv2* out2 = reinterpret_cast<dv2*>(out + h);
-    for (int t = tid; t < np; t += 256) {
-      dv2 v;
-      if (h) { v.x = acc[1 + 2 * t]; v.y = acc[2 + 2 * t]; }
-      else v = reinterpret_cast<const dv2*>(acc)[t];
-      __builtin_nontemporal_store(v, out2 + t);
+    // a batch's LDS reads are issued together, then its stores (one LDS latency per batch,
+    // not per store: the LDS is busy with other workgroups' atomics)
+    constexpr int SU = 4;
+    for (int t0 = tid; t0 < np; t0 += 256 * SU) {
+      dv2 v[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int t = t0 + 256 * u;
+        if (t < np) {
+          if (h) { v[u].x = acc[1 + 2 * t]; v[u].y = acc[2 + 2 * t]; }
+          else v[u] = reinterpret_cast<const dv2*>(acc)[t];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int t = t0 + 256 * u;
+        if (t < np) __builtin_nontemporal_store(v[u], out2 + t);
+      }
     }
     if (((nv - h) & 1) && tid == 0) __builtin_nontemporal_store(acc[nv - 1], out + nv - 1);
 #if FA_ABL == 8
     }
 #endif
   }
+  GT_MARK(gt_d);
+#if FA_GATHER_TIMING
+  gt[0] += gt_b - gt_top;
+  gt[1] += gt_c - gt_b;
+  gt[2] += gt_d - gt_c;
+  gt[6] += 1;
+#endif
   if (nchunk >= P.nchunks) break;
   __syncthreads();  // the store has read acc
-  if (!PIPE) fetch(nxt);
-  stage(nxt);
+  GT_MARK(gt_e);
+  zero_acc(nxt);
   cur = nxt;
   nxt = nn2;
   nchunk = nnchunk;
-  nnchunk = P.ctr ? s_idx[kpar] : chunk_of(vb + 3 * vstep);  // written before the items barrier
+  nnchunk = P.ctr ? (int64_t)__builtin_amdgcn_readfirstlane((int)s_idx[kpar])  // written before the items barrier
+                  : chunk_of(vb + 3 * vstep);
   kpar ^= 1;
   vb += vstep;
+  GT_MARK(gt_f);
   __syncthreads();
+#if FA_GATHER_TIMING
+  gt_top = __builtin_amdgcn_s_memtime();
+  gt[3] += gt_e - gt_d;
+  gt[4] += gt_f - gt_e;
+  gt[5] += gt_top - gt_f;
+#endif
   }
+#if FA_GATHER_TIMING
+  if ((tid & 63) == 0)
+    for (int k = 0; k < 7; ++k) atomicAdd(&g_gather_timing[k], gt[k]);
+#endif
 }
 
 // ------------------------------------------------------------------------------------ adjacency
@@ -2003,6 +2110,7 @@ static bool gather_dynamic() {
 
 static int chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
   int rc;
+  if (P.nchunks >= (1ll << 31)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks (>= 2^31)", (long long)P.nchunks);
   if ((rc = scratch_alloc((void**)buf, sizeof(int64_t) * (2 * (P.nchunks + 1) + 8), s))) return rc;
   P.chunk_b = *buf;
   P.chunk_a = *buf + (P.nchunks + 1);
@@ -2081,8 +2189,25 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     int64_t* desc = nullptr;
     if ((rc = chunk_desc(P, &desc, s))) return rc;
     const int64_t grid = gather_grid(k_gather<GD, NN, NV, NQ, NSPLIT, MAT>, P.nchunks);
+#if FA_GATHER_TIMING
+    {
+      unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_gather_timing), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
+    }
+#endif
     k_gather<GD, NN, NV, NQ, NSPLIT, MAT><<<(unsigned)grid, 256, 0, s>>>(P);
     LAUNCH_CHECK();
+#if FA_GATHER_TIMING
+    {
+      unsigned long long t[8];
+      HIP_TRY(hipMemcpyFromSymbolAsync(t, HIP_SYMBOL(g_gather_timing), sizeof(t), 0, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      const double n = (double)(t[6] ? t[6] : 1);
+      fprintf(stderr, "[gather timing] per wave-chunk (shader clocks): items %.0f | wait-items %.0f | store %.0f | "
+                      "wait-store %.0f | stage %.0f | wait-stage %.0f | wave-chunks %llu\n",
+              t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5] / n, t[6]);
+    }
+#endif
     HIP_TRY(hipFreeAsync(desc, s));
   }
   if (W.mode == GatherStage::FULL) {
