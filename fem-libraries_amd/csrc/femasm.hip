@@ -1073,7 +1073,7 @@ __device__ __forceinline__ void lds_add_block(double* acc, int s, double (&K)[GD
 #define FA_GATHER_TIMING 0  // 1: per-phase shader-clock totals of the gather (measurement build)
 #endif
 #if FA_GATHER_TIMING
-__device__ unsigned long long g_gather_timing[8];
+__device__ unsigned long long g_gather_timing[10];
 #define GT_MARK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #else
 #define GT_MARK(v)
@@ -1287,7 +1287,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   __syncthreads();
   int kpar = 0;
 #if FA_GATHER_TIMING
-  unsigned long long gt[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long gt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long gt_top = __builtin_amdgcn_s_memtime();
 #endif
   for (;;) {
@@ -1345,6 +1345,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   // the item body; FROMPF: the thread's first item, whose loads were issued during the
   // previous chunk (compile-time flag, so the prefetch registers die at its end)
   auto item = [&](const int it0, auto FROMPF) {
+    GT_MARK(gt_i0);
     const int part = it0 % NSPLIT;
     const int j = perm(it0 / NSPLIT, na, stride, inv_n);
     const int32_t pflat = s_adj[j];
@@ -1513,6 +1514,11 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       } else {
         lds_slots<NBG>(cols, lo, hi, cn, niter, sl);
       }
+#if FA_GATHER_TIMING
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const unsigned long long gt_i1 = __builtin_amdgcn_s_memtime();
+      gt[7] += gt_i1 - gt_i0;
+#endif
       const uint32_t rowm = (mask >> (aloc * GD)) & ((1u << GD) - 1);
       const double* Ah = s_ahat + (aloc * NN + part * NBG) * BS2;
 #pragma unroll FA_GATHER_UNROLL_B
@@ -1564,6 +1570,9 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
 #endif
         Ah += BS2;
       }
+#if FA_GATHER_TIMING
+      gt[8] += __builtin_amdgcn_s_memtime() - gt_i1;
+#endif
     } else {
       // non-affine tensor cells: J^-1 per quadrature point, read from the record as the rolled
       // q loop needs it; only the per-column accumulators G stay live
@@ -1764,7 +1773,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   }
 #if FA_GATHER_TIMING
   if ((tid & 63) == 0)
-    for (int k = 0; k < 7; ++k) atomicAdd(&g_gather_timing[k], gt[k]);
+    for (int k = 0; k < 9; ++k) atomicAdd(&g_gather_timing[k], gt[k]);
 #endif
 }
 
@@ -2191,7 +2200,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     const int64_t grid = gather_grid(k_gather<GD, NN, NV, NQ, NSPLIT, MAT>, P.nchunks);
 #if FA_GATHER_TIMING
     {
-      unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
       HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_gather_timing), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
     }
 #endif
@@ -2199,13 +2208,14 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     LAUNCH_CHECK();
 #if FA_GATHER_TIMING
     {
-      unsigned long long t[8];
+      unsigned long long t[10];
       HIP_TRY(hipMemcpyFromSymbolAsync(t, HIP_SYMBOL(g_gather_timing), sizeof(t), 0, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
       const double n = (double)(t[6] ? t[6] : 1);
       fprintf(stderr, "[gather timing] per wave-chunk (shader clocks): items %.0f | wait-items %.0f | store %.0f | "
-                      "wait-store %.0f | stage %.0f | wait-stage %.0f | wave-chunks %llu\n",
-              t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5] / n, t[6]);
+                      "wait-store %.0f | stage %.0f | wait-stage %.0f | wave-chunks %llu | item loads %.0f | "
+                      "item blocks %.0f\n",
+              t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5] / n, t[6], t[7] / n, t[8] / n);
     }
 #endif
     HIP_TRY(hipFreeAsync(desc, s));
