@@ -10,12 +10,15 @@ GPU owns a slab of cube layers [k0, k1) of an n_x x n_y x n_z box:
   the two interface planes (z = k0 and z = k1) carry the full global pattern on both neighbours;
 * rows are the lattice planes p*k0 .. p*k1 of the degree-p lattice (a fa_bsr row window); with
   lattice numbering each interface plane is one contiguous slab of BSR values;
-* the only exchange is, per slab boundary, ONE all-reduce(SUM) of that slab between the two
-  neighbouring ranks (a 2-rank process group: xGMI is point-to-point, a global all-reduce of all
-  interfaces would be link-bound — SURVEY.md §5). Boundaries are processed in two phases (even
-  pairs, then odd pairs) so the collectives of every rank are issued in a compatible order.
-* interface rows are owned by the lower rank (doc.tex:464); after the sum both copies are equal,
-  and Dirichlet diagonals on interface rows (inserted by both ranks) are reset to `diagonal`.
+* the only exchange is, per slab boundary, ONE all-reduce(SUM) between the two neighbouring
+  ranks (a 2-rank process group: xGMI is point-to-point, a global all-reduce of all interfaces
+  would be link-bound — SURVEY.md §5) of the interface rows' blocks in or above the plane (the
+  only ones the upper rank contributes to; ``interface_suffix``). Boundaries are processed in two
+  phases (even pairs, then odd pairs) so the collectives of every rank are issued in a compatible
+  order. The interface rows are assembled first and the all-reduces run on RCCL's stream while the
+  interior rows assemble (``SlabProblem.assemble``).
+* interface rows are owned by the lower rank (doc.tex:464), whose copy is complete after the sum;
+  Dirichlet diagonals on interface rows (inserted by both ranks) are reset to `diagonal`.
 
 The partition / numbering logic (``SlabPartition``) and the exchange (``exchange_interfaces``) are
 device-agnostic (torch tensors on any device, any torch.distributed backend: tested with gloo on
@@ -86,6 +89,24 @@ def interface_slices(part: SlabPartition, indptr: torch.Tensor):
     return out
 
 
+def interface_suffix(part: SlabPartition, indptr: torch.Tensor, indices: torch.Tensor) -> dict:
+    """Per interface plane: the window-relative block indices of its rows' blocks whose column lies
+    in the plane or above it. Lattice numbering is plane-major, so that is "column >= the plane's
+    first node". The rank above a plane contributes to those blocks only (its cells lie above), so
+    summing them gives the plane's owner -- the rank below (doc.tex:464) -- complete rows, while
+    about a third of each interface row (columns below the plane, the owner's alone) never
+    crosses the link. Both ranks select the same blocks in the same order (identical patterns)."""
+    base = int(indptr[part.row_begin])
+    out = {}
+    for name, rr in (("lower", part.lower), ("upper", part.upper)):
+        if rr is None:
+            continue
+        b0, b1 = int(indptr[rr[0]]), int(indptr[rr[1]])
+        sel = torch.nonzero(indices[b0:b1] >= rr[0]).flatten()
+        out[name] = (sel + (b0 - base)).to(torch.int64)
+    return out
+
+
 def bc_diagonal_fixups(part: SlabPartition, indptr: torch.Tensor, indices: torch.Tensor, marker: torch.Tensor | None,
                        bs: int) -> torch.Tensor | None:
     """Flat value indices (window-relative) of Dirichlet diagonal entries on interface rows."""
@@ -112,10 +133,13 @@ def bc_diagonal_fixups(part: SlabPartition, indptr: torch.Tensor, indices: torch
 
 
 def exchange_interfaces(part: SlabPartition, values: torch.Tensor, slices: dict, groups, fixups=None,
-                        diagonal: float = 1.0, async_op: bool = False):
+                        diagonal: float = 1.0, async_op: bool = False, suffix: dict | None = None):
     """Sum the interface-plane rows with the slab neighbours (2-rank all-reduces), then reset the
     Dirichlet diagonals of interface rows. `values` = the window's [nblocks_window, bs, bs].
 
+    suffix (``interface_suffix``): sum only the blocks the rank above a plane contributes to,
+    gathered into a contiguous buffer; the owner's rows are then complete (the non-owner's copy
+    of a plane keeps only that part). None: all-reduce whole interface rows (both copies equal).
     async_op: only issue the all-reduces (RCCL runs them on its own stream, after the work
     already queued on the current stream) and return a handle for ``finish_exchange``; the
     caller can queue the interior rows meanwhile."""
@@ -124,28 +148,36 @@ def exchange_interfaces(part: SlabPartition, values: torch.Tensor, slices: dict,
     flat = values.reshape(values.shape[0], -1)
     steps = []
     if part.lower is not None:
-        steps.append((part.rank - 1, slices["lower"]))  # boundary q = rank-1
+        steps.append((part.rank - 1, "lower"))  # boundary q = rank-1
     if part.upper is not None:
-        steps.append((part.rank, slices["upper"]))  # boundary q = rank
+        steps.append((part.rank, "upper"))  # boundary q = rank
     # phase order: even boundaries first, then odd — consistent on both sides of every boundary
-    works = []
-    for q, (b0, b1) in sorted(steps, key=lambda s: (s[0] % 2, s[0])):
-        slab = flat[b0:b1]
-        works.append(dist.all_reduce(slab, op=dist.ReduceOp.SUM, group=groups[q], async_op=async_op))
-    handle = (works, values, fixups, diagonal)
+    pending = []
+    for q, name in sorted(steps, key=lambda s: (s[0] % 2, s[0])):
+        if suffix is not None:
+            idx = suffix[name]
+            buf = flat.index_select(0, idx)
+        else:
+            b0, b1 = slices[name]
+            idx, buf = None, flat[b0:b1]
+        w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=groups[q], async_op=async_op)
+        pending.append((w, idx, buf))
+    handle = (pending, flat, values, fixups, diagonal)
     if async_op:
         return handle
-    finish_exchange(([], values, fixups, diagonal))
+    finish_exchange(handle)
     return None
 
 
 def finish_exchange(handle):
     """Wait for the all-reduces of ``exchange_interfaces(async_op=True)`` (the current stream waits
-    on RCCL's) and reset the Dirichlet diagonals of the interface rows."""
-    works, values, fixups, diagonal = handle
-    for w in works:
+    on RCCL's), scatter gathered sums back and reset the Dirichlet diagonals of the interface rows."""
+    pending, flat, values, fixups, diagonal = handle
+    for w, idx, buf in pending:
         if w is not None:
             w.wait()
+        if idx is not None:
+            flat.index_copy_(0, idx, buf)
     if fixups is not None:
         values.view(-1)[fixups] = diagonal
 
@@ -156,7 +188,7 @@ class SlabProblem:
     x = 1 prescribed. ``assemble()`` = local gather assembly + interface exchange."""
 
     def __init__(self, n: int, rank: int, world: int, device, degree: int = 2, nu: float = 0.3, groups=None,
-                 cell_type=None):
+                 cell_type=None, exchange: str = "suffix"):
         from . import fem, mesh
         from .la import MatrixCSR
         from .materials import e_range
@@ -195,6 +227,13 @@ class SlabProblem:
         self.split = fem.SplitGather(self.a, self.bcs, self.A, iface + [inner])
         self.n_iface = len(iface)
         self.slices = interface_slices(part, self.A.indptr)
+        self.suffix = interface_suffix(part, self.A.indptr, self.A.indices) if exchange == "suffix" else None
+        bs2 = 9
+        if self.suffix is not None:
+            nblk = sum(int(v.numel()) for v in self.suffix.values())
+        else:
+            nblk = sum(b1 - b0 for b0, b1 in self.slices.values())
+        self.exchange_bytes = 8 * bs2 * nblk  # values all-reduced per assembly by this rank
         self.fixups = bc_diagonal_fixups(part, self.A.indptr, self.A.indices, marker, 3)
         self.groups = groups if groups is not None else make_pair_groups(world)
         self.num_cells = m_asm.num_cells
@@ -210,9 +249,10 @@ class SlabProblem:
             sg.rows(i)
         if overlap:
             h = exchange_interfaces(self.part, self.A.parts[0][2], self.slices, self.groups, self.fixups,
-                                    async_op=True)
+                                    async_op=True, suffix=self.suffix)
             sg.rows(self.n_iface)
             finish_exchange(h)
         else:
             sg.rows(self.n_iface)
-            exchange_interfaces(self.part, self.A.parts[0][2], self.slices, self.groups, self.fixups)
+            exchange_interfaces(self.part, self.A.parts[0][2], self.slices, self.groups, self.fixups,
+                                suffix=self.suffix)

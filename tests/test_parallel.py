@@ -27,7 +27,7 @@ def _bc_marker(xs, bs):
     return on.repeat_interleave(bs).to(torch.int8)
 
 
-def _worker(rank, world, port, n, async_op=False):
+def _worker(rank, world, port, n, async_op=False, mode="rows"):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -60,11 +60,12 @@ def _worker(rank, world, port, n, async_op=False):
     slices = parallel.interface_slices(part, ip_t)
     fix = parallel.bc_diagonal_fixups(part, ip_t, ix_t, marker, bs)
     groups = parallel.make_pair_groups(world)
+    suffix = parallel.interface_suffix(part, ip_t, ix_t) if mode == "suffix" else None
     if async_op:  # the overlapped form SlabProblem.assemble uses: issue, (interior work), finish
-        h = parallel.exchange_interfaces(part, window, slices, groups, fix, async_op=True)
+        h = parallel.exchange_interfaces(part, window, slices, groups, fix, async_op=True, suffix=suffix)
         parallel.finish_exchange(h)
     else:
-        parallel.exchange_interfaces(part, window, slices, groups, fix)
+        parallel.exchange_interfaces(part, window, slices, groups, fix, suffix=suffix)
 
     # global reference
     m = mesh.create_unit_cube(n, n, n, ct)
@@ -82,14 +83,20 @@ def _worker(rank, world, port, n, async_op=False):
         gc = gix[gip[g]:gip[g + 1]]
         assert np.array_equal(lc, gc), f"rank {rank} row {r}: pattern differs"
         lv = window[int(indptr[r]) - w0:int(indptr[r + 1]) - w0].numpy()
-        err = max(err, float(np.abs(lv - gvals[gip[g]:gip[g + 1]]).max()))
+        gv = gvals[gip[g]:gip[g + 1]]
+        if mode == "suffix" and part.lower is not None and r < part.lower[1]:
+            keep = lc >= part.lower[0] + part.node_offset  # non-owned copy: the exchanged blocks only
+            lv, gv = lv[keep], gv[keep]
+        err = max(err, float(np.abs(lv - gv).max()))
     assert err <= 1e-12 * scale, f"rank {rank}: rel err {err / scale:.2e}"
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n,async_op", [(2, 4, False), (3, 5, False), (4, 4, False), (3, 5, True), (4, 4, True)])
-def test_slab_exchange_gloo(world, n, async_op):
-    mp.spawn(_worker, args=(world, _free_port(), n, async_op), nprocs=world, join=True)
+@pytest.mark.parametrize("world,n,async_op,mode", [(2, 4, False, "rows"), (3, 5, False, "rows"), (4, 4, False, "rows"),
+                                                   (3, 5, True, "rows"), (2, 4, False, "suffix"),
+                                                   (4, 4, True, "suffix"), (3, 5, True, "suffix")])
+def test_slab_exchange_gloo(world, n, async_op, mode):
+    mp.spawn(_worker, args=(world, _free_port(), n, async_op, mode), nprocs=world, join=True)
 
 
 def test_slab_partition_covers_all_layers():
