@@ -1078,6 +1078,9 @@ __device__ unsigned long long g_gather_timing[10];
 #else
 #define GT_MARK(v)
 #endif
+#ifndef FA_GATHER_AHAT_GLOBAL
+#define FA_GATHER_AHAT_GLOBAL 0  // 1: reference tensor read through the vector L1 instead of LDS
+#endif
 #ifndef FA_GATHER_CN_ALWAYS
 #define FA_GATHER_CN_ALWAYS 0
 #endif
@@ -1103,7 +1106,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   constexpr bool TAB = (MAT != MAT_BLOCKS) && (NEO || !SIMP);  // quadrature tables staged in LDS
   __shared__ double s_w[TAB ? NQ : 1];
   __shared__ double s_dphi[TAB ? NQ * NN * GD : 1];
-  __shared__ double s_ahat[SIMP ? NN * NN * BS2 : 1];
+  __shared__ double s_ahat[SIMP && !FA_GATHER_AHAT_GLOBAL ? NN * NN * BS2 : 1];
 
   const int tid = threadIdx.x;
   const int64_t abase = sload(P.A.indptr, P.A.row_begin);  // block index of the window's first value
@@ -1163,8 +1166,9 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   } else if constexpr (NEO) {
     for (int t = tid; t < NQ; t += 256) s_w[t] = P.tab[t];
     for (int t = tid; t < NQ * NN * GD; t += 256) s_dphi[t] = P.tab[NQ + t];
-  } else if constexpr (SIMP) {
+  } else if constexpr (SIMP && !FA_GATHER_AHAT_GLOBAL) {
     for (int t = tid; t < NN * NN * BS2; t += 256) s_ahat[t] = P.ahat[t];
+  } else if constexpr (SIMP) {
   } else {
     for (int t = tid; t < NQ; t += 256) s_w[t] = P.tab[t];
     for (int t = tid; t < NQ * NN * GD; t += 256) s_dphi[t] = P.tab[NQ + t];
@@ -1520,7 +1524,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       gt[7] += gt_i1 - gt_i0;
 #endif
       const uint32_t rowm = (mask >> (aloc * GD)) & ((1u << GD) - 1);
-      const double* Ah = s_ahat + (aloc * NN + part * NBG) * BS2;
+      const double* Ah = (FA_GATHER_AHAT_GLOBAL ? P.ahat : s_ahat) + (aloc * NN + part * NBG) * BS2;
 #pragma unroll FA_GATHER_UNROLL_B
       for (int bb = 0; bb < NBG; ++bb) {
         const int b = part * NBG + bb;
