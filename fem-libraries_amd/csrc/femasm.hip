@@ -861,6 +861,7 @@ struct GatherArgs {
   int64_t nchunks;
   unsigned long long* ctr;  // [8] per-XCD chunk counters (dynamic persistent grid), or NULL
   const uint16_t* slots;  // optional [adjacency entry][NN] position of the block within its row
+  int slot_order;         // 0, or the NSPLIT whose item order fa_plan_order baked into `slots`
   const int8_t* bc;
   double diag;
   const double* tab;  // device tables: wq | dphi | gdphi
@@ -1090,6 +1091,21 @@ __device__ unsigned long long g_gather_timing[10];
 #ifndef FA_GATHER_PIPE_NEO
 #define FA_GATHER_PIPE_NEO 0
 #endif
+// Item -> lane order of the gather: consecutive adjacency entries belong to the same row and add
+// into the same LDS slots, so entry jj of a chunk with na entries goes to position
+// (jj * stride) mod na, stride coprime to na; (x * stride) mod na in 32-bit with a float
+// quotient estimate (x < 2^24: off by <= 1). Shared by k_gather and the plan's k_order_slots.
+__device__ __forceinline__ int gather_perm_stride(int na) {
+  int st = 97;
+  while (na % st == 0 && st > 1) st -= 2;
+  return st;
+}
+__device__ __forceinline__ int gather_perm(int jj, int na, int st, float inv) {
+  const int x = jj * st;
+  int j = x - na * (int)((float)x * inv);
+  return j < 0 ? j + na : (j >= na ? j - na : j);
+}
+
 template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT>
 __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   using R = Rec<GD, NV, NQ, MAT>;
@@ -1259,16 +1275,10 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   // record). (jp * stride) mod na in 32-bit with a float quotient estimate (x < 2^24: off by <= 1).
   // (neo-Hookean: measured 3 % faster without the permutation, n = 120)
   constexpr bool PERM = FA_GATHER_PERMUTE && !NEO;
-  auto perm_stride = [&](int na_) {
-    int st = 97;
-    while (PERM && na_ % st == 0 && st > 1) st -= 2;
-    return st;
-  };
+  auto perm_stride = [&](int na_) { return PERM ? gather_perm_stride(na_) : 1; };
   auto perm = [&](int jj, int na_, int st, float inv) {
     if constexpr (!PERM) return jj;
-    const int x = jj * st;
-    int j_ = x - na_ * (int)((float)x * inv);
-    return j_ < 0 ? j_ + na_ : (j_ >= na_ ? j_ - na_ : j_);
+    return gather_perm(jj, na_, st, inv);
   };
   // Item prefetch (affine-simplex records): the first item of a thread in the NEXT chunk is
   // loaded after this chunk's items, so its latency hides behind the store / stage / barriers
@@ -1508,9 +1518,21 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       // affine simplex: G_ab = |J| Ji^T Ahat_ab Ji  (reference-tensor form)
       const double wdet = r[BS2], lam = r[BS2 + 1] * wdet, mu = r[BS2 + 2] * wdet;
       int sl[NBG];  // slots of the item's column nodes, searched together
+      // their local column indices b, 6 bits each (the plan's order when slot_order is set)
+      static_assert(NBG * 6 <= 64 && NN <= 64, "packed column list");
+      uint64_t bcp = 0;
+#pragma unroll
+      for (int bb = 0; bb < NBG; ++bb) bcp |= (uint64_t)(part * NBG + bb) << (6 * bb);
       if (decltype(FROMPF)::value && P.slots) {  // prefetched slot offsets
 #pragma unroll
         for (int bb = 0; bb < NBG; ++bb) sl[bb] = lo + cn[bb];
+      } else if (P.slots && P.slot_order) {  // (b << 10) | position, in bank-conflict-aware order
+#pragma unroll
+        for (int bb = 0; bb < NBG; ++bb) {
+          const int v = (int)P.slots[(a0 + j) * NN + part * NBG + bb];
+          sl[bb] = lo + (v & 1023);
+          bcp = (bcp & ~((uint64_t)63 << (6 * bb))) | ((uint64_t)(v >> 10) << (6 * bb));
+        }
       } else if (P.slots) {
 #pragma unroll
         for (int bb = 0; bb < NBG; ++bb)
@@ -1524,11 +1546,13 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       gt[7] += gt_i1 - gt_i0;
 #endif
       const uint32_t rowm = (mask >> (aloc * GD)) & ((1u << GD) - 1);
-      const double* Ah = (FA_GATHER_AHAT_GLOBAL ? P.ahat : s_ahat) + (aloc * NN + part * NBG) * BS2;
+      const double* Ah0 = (FA_GATHER_AHAT_GLOBAL ? P.ahat : s_ahat) + aloc * NN * BS2;
 #pragma unroll FA_GATHER_UNROLL_B
       for (int bb = 0; bb < NBG; ++bb) {
-        const int b = part * NBG + bb;
-        if (NN % NSPLIT != 0 && b >= NN) break;
+        if (NN % NSPLIT != 0 && part * NBG + bb >= NN) break;
+        const int b = (int)(bcp & 63);  // rolled loop: shift the column list like the slot list
+        bcp >>= 6;
+        const double* Ah = Ah0 + b * BS2;
 #if FA_ABL == 4
         double Ahr[BS2];
 #pragma unroll
@@ -1572,7 +1596,6 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
 #else
         lds_add_block<GD>(acc, s, K, rowm, (mask >> (b * GD)) & ((1u << GD) - 1));
 #endif
-        Ah += BS2;
       }
 #if FA_GATHER_TIMING
       gt[8] += __builtin_amdgcn_s_memtime() - gt_i1;
@@ -1650,7 +1673,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   if (abl_sink == 1.2345) acc[0] = abl_sink;
 #endif
   have_pf = false;
-  if (IPF && nchunk < P.nchunks) {
+  if (IPF && nchunk < P.nchunks && !P.slot_order) {
     have_pf = true;
     const int na_n = (int)(nxt.a1 - nxt.a0);
     if (tid < na_n * NSPLIT) {
@@ -2015,6 +2038,130 @@ extern "C" int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const
   if (herr & 8) return fail(FA_E_CAPACITY, "a row holds more than 65535 blocks");
   if (herr) return fail(FA_E_PATTERN, "sparsity pattern misses a (row, column) pair of a cell");
   plan->slots = slots;
+  plan->slot_order = 0;
+  return FA_OK;
+}
+
+// Bank-conflict-aware item order (fa_plan_order). An item's NBG blocks are added one per step of
+// its rolled block loop, 9 ds_add_f64 each; the lanes of a 32-lane half-wave conflict when their
+// slots are equal mod 32 (72-B blocks: dword address 18*slot + 2e, 64 banks). Within each
+// half-wave of the kernel's item -> lane mapping, the order in which every lane visits its NBG
+// column slots is chosen greedily so that each step's 32 slots spread over the residues (ties:
+// residues mod 16 inside each 16-lane quarter). The slot map then holds (b << 10) | position in
+// that order. One thread per (chunk, half-wave).
+template <int NN, int NSPLIT>
+__global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64_t* __restrict__ indptr,
+                              const int64_t* __restrict__ adj_ptr, int64_t nchunks, int groups_per_chunk,
+                              uint16_t* __restrict__ slots) {
+  constexpr int NBG = NN / NSPLIT;
+  const int64_t total = nchunks * groups_per_chunk;
+  for (int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gid < total;
+       gid += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = gid / groups_per_chunk;
+    const int g = (int)(gid % groups_per_chunk);
+    const int64_t r0 = row_start[c], r1 = row_start[c + 1];
+    const int64_t a0 = adj_ptr[r0];
+    const int na = (int)(adj_ptr[r1] - a0);
+    const int nitems = na * NSPLIT;
+    const int p0 = 32 * g;
+    if (p0 >= nitems) continue;
+    const int64_t b0 = indptr[r0];
+    const int st = gather_perm_stride(na);
+    const float inv = 1.0f / (float)na;
+    const int nl = min(32, nitems - p0);
+    uint16_t off[32][NBG];
+    uint8_t res[32][NBG];
+    int64_t ent[32];
+    uint32_t used[32];
+    for (int q = 0; q < nl; ++q) {
+      const int p = p0 + q;
+      const int part = p % NSPLIT;
+      const int j = gather_perm(p / NSPLIT, na, st, inv);
+      const int64_t e = a0 + j;
+      int64_t lo = r0, hi = r1 - 1;  // row of entry e: adj_ptr[row] <= e < adj_ptr[row + 1]
+      while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (adj_ptr[mid] <= e) lo = mid; else hi = mid - 1;
+      }
+      const int rowlo = (int)(indptr[lo] - b0);
+      ent[q] = e * NN + part * NBG;
+      used[q] = 0u;
+      for (int t = 0; t < NBG; ++t) {
+        off[q][t] = slots[ent[q] + t];
+        res[q][t] = (uint8_t)((rowlo + off[q][t]) & 31);
+      }
+    }
+    uint8_t pick[32][NBG];
+    for (int t = 0; t < NBG; ++t) {
+      uint8_t cnt32[32], cnt16[2][16];
+      for (int k = 0; k < 32; ++k) cnt32[k] = 0;
+      for (int k = 0; k < 16; ++k) cnt16[0][k] = cnt16[1][k] = 0;
+      for (int q = 0; q < nl; ++q) {
+        int best = -1, bc = 1 << 30;
+        for (int k = 0; k < NBG; ++k) {
+          if ((used[q] >> k) & 1u) continue;
+          const int r = res[q][k];
+          const int cost = 64 * cnt32[r] + cnt16[(q >> 4) & 1][r & 15];
+          if (cost < bc) { bc = cost; best = k; }
+        }
+        used[q] |= 1u << best;
+        pick[q][t] = (uint8_t)best;
+        ++cnt32[res[q][best]];
+        ++cnt16[(q >> 4) & 1][res[q][best] & 15];
+      }
+    }
+    for (int q = 0; q < nl; ++q) {
+      const int part = (p0 + q) % NSPLIT;
+      uint16_t v[NBG];
+      for (int t = 0; t < NBG; ++t) {
+        const int k = pick[q][t];
+        v[t] = (uint16_t)(((part * NBG + k) << 10) | off[q][k]);
+      }
+      for (int t = 0; t < NBG; ++t) slots[ent[q] + t] = v[t];
+    }
+  }
+}
+
+// NSPLIT of the affine-simplex linear-elasticity gather kernel for (cell, degree, quadrature
+// points), or 0 when that kernel does not exist (must match dispatch_gather)
+#ifndef FA_P2TET_NSPLIT
+#define FA_P2TET_NSPLIT 2  // measured best with the reference-tensor blocks (n=120 sweep, DESIGN.md)
+#endif
+static int lin_simplex_nsplit(int ct, int p, int nq) {
+  if (ct == FA_TRIANGLE && p == 1 && nq == 1) return 1;
+  if (ct == FA_TRIANGLE && p == 2 && nq == 3) return 2;
+  if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return 2;
+  if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return FA_P2TET_NSPLIT;
+  return 0;
+}
+
+extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, fa_plan* plan,
+                             void* stream) {
+  int rc = check_mesh(mesh);
+  if (rc) return rc;
+  if (!adj || !A || !plan) return fail(FA_E_ARG, "null argument");
+  if (!plan->slots) return fail(FA_E_ARG, "fa_plan_order needs the slot map (fa_plan_slots first)");
+  plan->slot_order = 0;
+  DevTables T;
+  if ((rc = get_tables(mesh->cell_type, mesh->degree, -1, &T))) return rc;
+  const int ns = lin_simplex_nsplit(mesh->cell_type, mesh->degree, T.nq);
+  if (ns == 0 || plan->nchunks <= 0) return FA_OK;  // no kernel reads an ordered map: keep plain slots
+  const int groups = (kGatherMaxAdj * ns + 31) / 32;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t total = plan->nchunks * groups;
+  uint16_t* sl = const_cast<uint16_t*>(plan->slots);
+#define ORD(NN_, NS_) k_order_slots<NN_, NS_><<<grid_for(total), 256, 0, s>>>(plan->row_start, A->indptr, adj->ptr, plan->nchunks, groups, sl)
+  if (mesh->nn == 3 && ns == 1) ORD(3, 1);
+  else if (mesh->nn == 6 && ns == 2) ORD(6, 2);
+  else if (mesh->nn == 4 && ns == 2) ORD(4, 2);
+  else if (mesh->nn == 10 && ns == 2) ORD(10, 2);
+  else if (mesh->nn == 10 && ns == 5) ORD(10, 5);
+  else if (mesh->nn == 10 && ns == 1) ORD(10, 1);
+  else return FA_OK;
+#undef ORD
+  LAUNCH_CHECK();
+  HIP_TRY(hipStreamSynchronize(s));
+  plan->slot_order = ns;
   return FA_OK;
 }
 
@@ -2064,6 +2211,7 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
   plan->max_blocks = mb;
   plan->max_adj = ma;
   plan->slots = nullptr;
+  plan->slot_order = 0;
   return FA_OK;
 }
 
@@ -2175,6 +2323,12 @@ static inline int64_t align256(int64_t b) { return (b + 255) & ~int64_t(255); }
 template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT>
 static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const GatherStage& W) {
   using R = Rec<GD, NV, NQ, MAT>;
+  // ordered (packed) slots are read only by the affine-simplex linear kernel of the same NSPLIT;
+  // any other kernel searches its slots in LDS instead
+  if (P.slot_order && !(MAT == 0 && R::SIMP && NN % NSPLIT == 0 && P.slot_order == NSPLIT)) {
+    P.slots = nullptr;
+    P.slot_order = 0;
+  }
   static_assert(NN * GD <= 32, "bc mask holds 32 dofs");
   const int64_t nc = P.M.ncells;
   const int64_t rec_bytes = align256((int64_t)sizeof(double) * R::SIZE * nc);
@@ -2234,14 +2388,15 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
 #ifndef FA_NEO_NSPLIT
 #define FA_NEO_NSPLIT 10  // measured (n=120 sweep): 10 > 5 > 2
 #endif
-#ifndef FA_P2TET_NSPLIT
-#define FA_P2TET_NSPLIT 2  // measured best with the reference-tensor blocks (n=120 sweep, DESIGN.md)
-#endif
 // Hexahedra: MFMA element blocks into a stream-ordered block store, then the row gather sums
 // them (the "store pass + per-destination sum pass" alternative to global atomics).
 template <int NN, int NQ, int NSPLIT>
 static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc, hipStream_t s, const GatherStage& W) {
   const int64_t nc = P.M.ncells;
+  if (P.slot_order) {
+    P.slots = nullptr;
+    P.slot_order = 0;
+  }
   if (W.mode == GatherStage::SIZE) {
     *W.bytes = align256((int64_t)sizeof(double) * 9 * NN * NN * nc);
     return FA_OK;
@@ -2374,6 +2529,7 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     P.M = M; P.F = F; P.A = Av;
     P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks;
     P.slots = plan->slots;
+    P.slot_order = plan->slots ? plan->slot_order : 0;
     P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr;
     bool handled = false;
     rc = dispatch_gather(mesh, T, F.kind, P, bc, s, &handled);
@@ -2446,6 +2602,7 @@ static int gather_stage(const fa_mesh* mesh, const fa_form* form, const fa_adjac
     P.A = BsrView{A->indptr, A->indices, A->data, wb, we};
     P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks;
     P.slots = plan->slots;
+    P.slot_order = plan->slots ? plan->slot_order : 0;
   }
   bool handled = false;
   rc = dispatch_gather(mesh, T, F.kind, P, bc, s, &handled, W);

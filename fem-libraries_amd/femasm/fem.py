@@ -494,6 +494,10 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0):
             slots = torch.empty(V.mesh.num_cells * V.nn * V.nn, dtype=torch.int16, device=V.mesh.device)
             _lib.check(L.fa_plan_slots(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), slots.data_ptr(),
                                        ctypes.byref(plan), sh), "fa_plan_slots")
+            # bank-conflict-aware block order for the affine-simplex kernels (FEMASM_SLOT_ORDER=0: off)
+            if os.environ.get("FEMASM_SLOT_ORDER", "1") != "0":
+                _lib.check(L.fa_plan_order(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), ctypes.byref(plan),
+                                           sh), "fa_plan_order")
         plans[key] = (plan, rs, A.indptr, slots)
     return plans[key][0]
 
@@ -567,12 +571,21 @@ class SplitGather:
             if r1 > r0:
                 _lib.check(L.fa_plan_gather(ctypes.byref(self.fm), ctypes.byref(self.adj), ctypes.byref(fb),
                                             rs.data_ptr(), ctypes.byref(plan), self.sh), "fa_plan_gather")
-                if self.slots is not None:
-                    _lib.check(L.fa_plan_slots(ctypes.byref(self.fm), ctypes.byref(self.adj), ctypes.byref(fb),
-                                               self.slots.data_ptr(), ctypes.byref(plan), self.sh), "fa_plan_slots")
             self.subs.append(fb)
             self.plans.append(plan)
             self._keep.append(rs)
+        if self.slots is not None:
+            # one slot map for all rows (fa_plan_slots writes every row), then each plan's order
+            live = [i for i, (r0, r1) in enumerate(ranges) if r1 > r0]
+            for i in live[:1]:
+                _lib.check(L.fa_plan_slots(ctypes.byref(self.fm), ctypes.byref(self.adj), ctypes.byref(self.subs[i]),
+                                           self.slots.data_ptr(), ctypes.byref(self.plans[i]), self.sh), "fa_plan_slots")
+            for i in live:
+                self.plans[i].slots = self.slots.data_ptr()
+                self.plans[i].slot_order = 0
+                if os.environ.get("FEMASM_SLOT_ORDER", "1") != "0":
+                    _lib.check(L.fa_plan_order(ctypes.byref(self.fm), ctypes.byref(self.adj), ctypes.byref(self.subs[i]),
+                                               ctypes.byref(self.plans[i]), self.sh), "fa_plan_order")
 
     def prepare(self):
         _lib.check(self.L.fa_gather_prepare(ctypes.byref(self.fm), ctypes.byref(self.ff), _lib.ptr(self.marker),

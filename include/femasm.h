@@ -114,6 +114,9 @@ typedef struct {
   int32_t max_adj;           /* largest adjacency count of a chunk */
   const uint16_t* slots;     /* optional device [ncells*nn][nn]: for adjacency entry j and column
                                 node b, the block's position within row j's column list */
+  int32_t slot_order;        /* 0: `slots` is that plain map; > 0: fa_plan_order rewrote it for the
+                                gather's item order (value = the kernel's column split) */
+  int32_t _pad;
 } fa_plan;
 
 const char* fa_last_error(void);
@@ -141,6 +144,14 @@ int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A
  * Fails with FA_E_CAPACITY if a row holds more than 65535 blocks. */
 int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, uint16_t* slots, fa_plan* plan,
                   void* stream);
+
+/* Bank-conflict-aware order for the gather's LDS adds (affine simplices, linear elasticity):
+ * rewrites plan->slots in place so that, for each group of 32 lanes of the kernel's item
+ * mapping, every lane visits its blocks in an order that spreads each step's LDS addresses over
+ * the banks; entries then hold (b << 10) | position. Sets plan->slot_order; a no-op (slot_order 0)
+ * for elements whose gather does not read an ordered map. Run after fa_plan_slots for EVERY
+ * plan sharing the slot map (fa_plan_slots rewrites all rows). */
+int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, fa_plan* plan, void* stream);
 
 /* Per-cell element matrices Ae [ncells_out][nn*bs][nn*bs] (dof = node*bs + comp) for cells
  * [c0, c0+ncells_out) — the batched ufcx tabulate_tensor / AssembleElementGrad. */
