@@ -2043,17 +2043,20 @@ extern "C" int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const
 }
 
 // Bank-conflict-aware item order (fa_plan_order). An item's NBG blocks are added one per step of
-// its rolled block loop, 9 ds_add_f64 each; the lanes of a 32-lane half-wave conflict when their
-// slots are equal mod 32 (72-B blocks: dword address 18*slot + 2e, 64 banks). Within each
-// half-wave of the kernel's item -> lane mapping, the order in which every lane visits its NBG
-// column slots is chosen greedily so that each step's 32 slots spread over the residues (ties:
-// residues mod 16 inside each 16-lane quarter). The slot map then holds (b << 10) | position in
-// that order. One thread per (chunk, half-wave).
+// its rolled block loop, 9 ds_add_f64 each, all lanes of a wave at the same step. Measured LDS
+// model (tools/probe/lds_bank_probe.hip, gfx950): a 64-bit LDS op serves each 16-lane quarter of
+// the wave on its own, and two lanes of a quarter conflict when their slots are equal mod 16
+// (72-B blocks); k lanes on one residue cost k passes, lanes on one slot a little more. Within each
+// quarter of the kernel's item -> lane mapping the order in which every lane visits its NBG column
+// slots is chosen to minimise sum over steps of the largest residue count (the passes), with the
+// sum of squared counts as tie-break: identity start, then pairwise step swaps per lane until no
+// swap improves. The slot map then holds (b << 10) | position in that order. One thread per
+// (chunk, quarter). stats (optional): {passes, identity passes, lower bound} summed.
 template <int NN, int NSPLIT>
 __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64_t* __restrict__ indptr,
                               const int64_t* __restrict__ adj_ptr, int64_t nchunks, int groups_per_chunk,
-                              uint16_t* __restrict__ slots) {
-  constexpr int NBG = NN / NSPLIT;
+                              uint16_t* __restrict__ slots, unsigned long long* __restrict__ stats) {
+  constexpr int NBG = NN / NSPLIT, Q = 16;
   const int64_t total = nchunks * groups_per_chunk;
   for (int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gid < total;
        gid += (int64_t)gridDim.x * blockDim.x) {
@@ -2063,16 +2066,20 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
     const int64_t a0 = adj_ptr[r0];
     const int na = (int)(adj_ptr[r1] - a0);
     const int nitems = na * NSPLIT;
-    const int p0 = 32 * g;
+    const int p0 = Q * g;
     if (p0 >= nitems) continue;
     const int64_t b0 = indptr[r0];
     const int st = gather_perm_stride(na);
     const float inv = 1.0f / (float)na;
-    const int nl = min(32, nitems - p0);
-    uint16_t off[32][NBG];
-    uint8_t res[32][NBG];
-    int64_t ent[32];
-    uint32_t used[32];
+    const int nl = min(Q, nitems - p0);
+    uint16_t off[Q][NBG];
+    uint8_t res[Q][NBG], pick[Q][NBG];
+    uint8_t cnt[NBG][16];
+    int64_t ent[Q];
+    for (int t = 0; t < NBG; ++t)
+      for (int r = 0; r < 16; ++r) cnt[t][r] = 0;
+    int deg[16];
+    for (int r = 0; r < 16; ++r) deg[r] = 0;
     for (int q = 0; q < nl; ++q) {
       const int p = p0 + q;
       const int part = p % NSPLIT;
@@ -2085,30 +2092,51 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
       }
       const int rowlo = (int)(indptr[lo] - b0);
       ent[q] = e * NN + part * NBG;
-      used[q] = 0u;
       for (int t = 0; t < NBG; ++t) {
         off[q][t] = slots[ent[q] + t];
-        res[q][t] = (uint8_t)((rowlo + off[q][t]) & 31);
+        res[q][t] = (uint8_t)((rowlo + off[q][t]) & 15);
+        pick[q][t] = (uint8_t)t;
+        ++cnt[t][res[q][t]];
+        ++deg[res[q][t]];
       }
     }
-    uint8_t pick[32][NBG];
-    for (int t = 0; t < NBG; ++t) {
-      uint8_t cnt32[32], cnt16[2][16];
-      for (int k = 0; k < 32; ++k) cnt32[k] = 0;
-      for (int k = 0; k < 16; ++k) cnt16[0][k] = cnt16[1][k] = 0;
-      for (int q = 0; q < nl; ++q) {
-        int best = -1, bc = 1 << 30;
-        for (int k = 0; k < NBG; ++k) {
-          if ((used[q] >> k) & 1u) continue;
-          const int r = res[q][k];
-          const int cost = 64 * cnt32[r] + cnt16[(q >> 4) & 1][r & 15];
-          if (cost < bc) { bc = cost; best = k; }
-        }
-        used[q] |= 1u << best;
-        pick[q][t] = (uint8_t)best;
-        ++cnt32[res[q][best]];
-        ++cnt16[(q >> 4) & 1][res[q][best] & 15];
-      }
+    auto step_max = [&](int t) {
+      int m = 0;
+      for (int r = 0; r < 16; ++r) m = max(m, (int)cnt[t][r]);
+      return m;
+    };
+    int ident = 0, lb = NBG, dmax = 0;
+    for (int t = 0; t < NBG; ++t) ident += step_max(t);
+    for (int r = 0; r < 16; ++r) dmax = max(dmax, deg[r]);
+    lb = max(lb, dmax);
+    for (int pass = 0; pass < 64; ++pass) {
+      bool improved = false;
+      for (int q = 0; q < nl; ++q)
+        for (int t1 = 0; t1 < NBG; ++t1)
+          for (int t2 = t1 + 1; t2 < NBG; ++t2) {
+            const int ra = res[q][pick[q][t1]], rb = res[q][pick[q][t2]];
+            if (ra == rb) continue;
+            const int m1 = step_max(t1), m2 = step_max(t2);
+            const int sq = 2 * (cnt[t1][rb] - cnt[t1][ra]) + 2 + 2 * (cnt[t2][ra] - cnt[t2][rb]) + 2;
+            --cnt[t1][ra]; ++cnt[t1][rb]; --cnt[t2][rb]; ++cnt[t2][ra];
+            const int d = step_max(t1) + step_max(t2) - m1 - m2;
+            if (d < 0 || (d == 0 && sq < 0)) {
+              const uint8_t x = pick[q][t1];
+              pick[q][t1] = pick[q][t2];
+              pick[q][t2] = x;
+              improved = true;
+            } else {
+              ++cnt[t1][ra]; --cnt[t1][rb]; ++cnt[t2][rb]; --cnt[t2][ra];
+            }
+          }
+      if (!improved) break;
+    }
+    if (stats) {
+      int cost = 0;
+      for (int t = 0; t < NBG; ++t) cost += step_max(t);
+      atomicAdd(stats + 0, (unsigned long long)cost);
+      atomicAdd(stats + 1, (unsigned long long)ident);
+      atomicAdd(stats + 2, (unsigned long long)lb);
     }
     for (int q = 0; q < nl; ++q) {
       const int part = (p0 + q) % NSPLIT;
@@ -2146,20 +2174,38 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   if ((rc = get_tables(mesh->cell_type, mesh->degree, -1, &T))) return rc;
   const int ns = lin_simplex_nsplit(mesh->cell_type, mesh->degree, T.nq);
   if (ns == 0 || plan->nchunks <= 0) return FA_OK;  // no kernel reads an ordered map: keep plain slots
-  const int groups = (kGatherMaxAdj * ns + 31) / 32;
+  const int groups = (kGatherMaxAdj * ns + 15) / 16;
   hipStream_t s = (hipStream_t)stream;
   const int64_t total = plan->nchunks * groups;
   uint16_t* sl = const_cast<uint16_t*>(plan->slots);
-#define ORD(NN_, NS_) k_order_slots<NN_, NS_><<<grid_for(total), 256, 0, s>>>(plan->row_start, A->indptr, adj->ptr, plan->nchunks, groups, sl)
+  // FA_ORDER_STATS=1: print the LDS passes of the accumulate steps (ordered / identity / bound)
+  const char* ev = getenv("FA_ORDER_STATS");
+  unsigned long long* st = nullptr;
+  if (ev && ev[0] == '1') {
+    HIP_TRY(hipMallocAsync((void**)&st, 3 * sizeof(unsigned long long), s));
+    HIP_TRY(hipMemsetAsync(st, 0, 3 * sizeof(unsigned long long), s));
+  }
+#define ORD(NN_, NS_) k_order_slots<NN_, NS_><<<grid_for(total), 256, 0, s>>>(plan->row_start, A->indptr, adj->ptr, plan->nchunks, groups, sl, st)
   if (mesh->nn == 3 && ns == 1) ORD(3, 1);
   else if (mesh->nn == 6 && ns == 2) ORD(6, 2);
   else if (mesh->nn == 4 && ns == 2) ORD(4, 2);
   else if (mesh->nn == 10 && ns == 2) ORD(10, 2);
   else if (mesh->nn == 10 && ns == 5) ORD(10, 5);
   else if (mesh->nn == 10 && ns == 1) ORD(10, 1);
-  else return FA_OK;
+  else {
+    if (st) (void)hipFreeAsync(st, s);
+    return FA_OK;
+  }
 #undef ORD
   LAUNCH_CHECK();
+  if (st) {
+    unsigned long long h[3];
+    HIP_TRY(hipMemcpyAsync(h, st, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipFreeAsync(st, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    fprintf(stderr, "fa_plan_order: LDS passes ordered %llu identity %llu bound %llu (%.3f / %.3f of identity)\n", h[0],
+            h[1], h[2], (double)h[0] / (double)h[1], (double)h[2] / (double)h[1]);
+  }
   HIP_TRY(hipStreamSynchronize(s));
   plan->slot_order = ns;
   return FA_OK;
