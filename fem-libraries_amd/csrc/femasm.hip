@@ -862,6 +862,10 @@ struct GatherArgs {
   unsigned long long* ctr;  // [8] per-XCD chunk counters (dynamic persistent grid), or NULL
   const uint16_t* slots;  // optional [adjacency entry][NN] position of the block within its row
   int slot_order;         // 0, or the NSPLIT whose item order fa_plan_order baked into `slots`
+  // positional plan (fa_plan_order with an entry buffer): each chunk's adjacency entries in the
+  // plan's bank-balanced order; `slots` is then indexed by that position and holds chunk-relative
+  // block positions, so items need neither the entry permutation nor their row
+  const int32_t* eadj;
   const int8_t* bc;
   double diag;
   const double* tab;  // device tables: wq | dphi | gdphi
@@ -1207,6 +1211,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   uint32_t pbc[GD];  // raw constrained-dof bytes of row tid, combined in stage
   const uint32_t* indptr_lo = reinterpret_cast<const uint32_t*>(P.A.indptr);
   const uint32_t* adjptr_lo = reinterpret_cast<const uint32_t*>(P.adj_ptr);
+  const int32_t* adj_src = P.eadj ? P.eadj : P.adj_idx;  // positional plan: entries in its order
   // Loads at clamped indices, unconditionally and with no use of their values here: a
   // per-load "load or constant" select makes hipcc branch around each load and wait for it,
   // which serialises the prefetch; stage() ignores the lanes past the chunk's counts.
@@ -1230,7 +1235,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     }
     if (na_ > 0) {
 #pragma unroll
-      for (int k = 0; k < NPA; ++k) pj[k] = P.adj_idx[d.a0 + min(tid + 256 * k, na_ - 1)];
+      for (int k = 0; k < NPA; ++k) pj[k] = adj_src[d.a0 + min(tid + 256 * k, na_ - 1)];
     }
   };
   // Metadata of a chunk: registers -> LDS. Runs right after the previous chunk's items barrier
@@ -1275,6 +1280,8 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   // record). (jp * stride) mod na in 32-bit with a float quotient estimate (x < 2^24: off by <= 1).
   // (neo-Hookean: measured 3 % faster without the permutation, n = 120)
   constexpr bool PERM = FA_GATHER_PERMUTE && !NEO;
+  // kernels that can run a positional plan (the ordered-slot affine-simplex elasticity path)
+  constexpr bool POSM = MAT == 0 && SIMP && NN % NSPLIT == 0;
   auto perm_stride = [&](int na_) { return PERM ? gather_perm_stride(na_) : 1; };
   auto perm = [&](int jj, int na_, int st, float inv) {
     if constexpr (!PERM) return jj;
@@ -1361,12 +1368,14 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   auto item = [&](const int it0, auto FROMPF) {
     GT_MARK(gt_i0);
     const int part = it0 % NSPLIT;
-    const int j = perm(it0 / NSPLIT, na, stride, inv_n);
+    // positional plan: entries are staged in the plan's order and slots are chunk-relative
+    const bool posm = POSM && P.eadj != nullptr;
+    const int j = posm ? it0 / NSPLIT : perm(it0 / NSPLIT, na, stride, inv_n);
     const int32_t pflat = s_adj[j];
     const int64_t c = pflat / NN;
     const int aloc = pflat % NN;
-    const int lr = adjrow[j];
-    const int lo = rowoff[lr], hi = rowoff[lr + 1];
+    const int lr = posm ? 0 : adjrow[j];
+    const int lo = posm ? 0 : rowoff[lr], hi = posm ? 0 : rowoff[lr + 1];
     // one record + the column nodes + the bc mask: all independent loads, issued together
     // registers: NEO keeps only Ji, wdet; tensor cells read their per-q records in the q loop
     constexpr int RL = NEO ? ((BS2 + 2) & ~1) : (SIMP || MAT == FA_ASYM_DAMAGE ? R::SIZE : 2);
@@ -2039,6 +2048,7 @@ extern "C" int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const
   if (herr) return fail(FA_E_PATTERN, "sparsity pattern misses a (row, column) pair of a cell");
   plan->slots = slots;
   plan->slot_order = 0;
+  plan->eadj = nullptr;
   return FA_OK;
 }
 
@@ -2052,10 +2062,13 @@ extern "C" int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const
 // sum of squared counts as tie-break: identity start, then pairwise step swaps per lane until no
 // swap improves. The slot map then holds (b << 10) | position in that order. One thread per
 // (chunk, quarter). stats (optional): {passes, identity passes, lower bound} summed.
+// Positional plans (eperm != NULL): position jj of a chunk holds entry eperm[a0 + jj]; the plain
+// map is read from src and written by position, with chunk-relative block positions.
 template <int NN, int NSPLIT>
 __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64_t* __restrict__ indptr,
                               const int64_t* __restrict__ adj_ptr, int64_t nchunks, int groups_per_chunk,
-                              uint16_t* __restrict__ slots, unsigned long long* __restrict__ stats) {
+                              uint16_t* __restrict__ slots, const uint16_t* __restrict__ src,
+                              const uint16_t* __restrict__ eperm, unsigned long long* __restrict__ stats) {
   constexpr int NBG = NN / NSPLIT, Q = 16;
   const int64_t total = nchunks * groups_per_chunk;
   for (int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gid < total;
@@ -2076,6 +2089,8 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
     uint8_t res[Q][NBG], pick[Q][NBG];
     uint8_t cnt[NBG][16];
     int64_t ent[Q];
+    int base[Q];
+    const uint16_t* rd = eperm ? src : slots;
     for (int t = 0; t < NBG; ++t)
       for (int r = 0; r < 16; ++r) cnt[t][r] = 0;
     int deg[16];
@@ -2083,7 +2098,7 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
     for (int q = 0; q < nl; ++q) {
       const int p = p0 + q;
       const int part = p % NSPLIT;
-      const int j = gather_perm(p / NSPLIT, na, st, inv);
+      const int j = eperm ? (int)eperm[a0 + p / NSPLIT] : gather_perm(p / NSPLIT, na, st, inv);
       const int64_t e = a0 + j;
       int64_t lo = r0, hi = r1 - 1;  // row of entry e: adj_ptr[row] <= e < adj_ptr[row + 1]
       while (lo < hi) {
@@ -2091,9 +2106,11 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
         if (adj_ptr[mid] <= e) lo = mid; else hi = mid - 1;
       }
       const int rowlo = (int)(indptr[lo] - b0);
-      ent[q] = e * NN + part * NBG;
+      base[q] = eperm ? rowlo : 0;
+      const int64_t ein = e * NN + part * NBG;
+      ent[q] = (eperm ? a0 + p / NSPLIT : e) * NN + part * NBG;
       for (int t = 0; t < NBG; ++t) {
-        off[q][t] = slots[ent[q] + t];
+        off[q][t] = rd[ein + t];
         res[q][t] = (uint8_t)((rowlo + off[q][t]) & 15);
         pick[q][t] = (uint8_t)t;
         ++cnt[t][res[q][t]];
@@ -2143,9 +2160,66 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
       uint16_t v[NBG];
       for (int t = 0; t < NBG; ++t) {
         const int k = pick[q][t];
-        v[t] = (uint16_t)(((part * NBG + k) << 10) | off[q][k]);
+        v[t] = (uint16_t)(((part * NBG + k) << 10) | (base[q] + off[q][k]));
       }
       for (int t = 0; t < NBG; ++t) slots[ent[q] + t] = v[t];
+    }
+  }
+}
+
+// Positional plan, step 1 (fa_plan_order with an entry buffer): which adjacency entries of a
+// chunk share a 16-lane quarter. Entries are placed one by one (in the kernel's default entry
+// permutation, which spreads rows) into the quarter with room whose residue histogram (slots
+// mod 16 over all its lanes' blocks) overlaps the entry's residues least, so that no residue
+// collects many more adds than the quarter has steps; the order search then spreads them over
+// the steps. Writes eperm (position -> entry offset) and eadj (the entries' adjacency values in
+// position order). One thread per chunk.
+template <int NN, int NSPLIT>
+__global__ void k_plan_perm(const int64_t* __restrict__ row_start, const int64_t* __restrict__ indptr,
+                            const int64_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj_idx,
+                            int64_t nchunks, const uint16_t* __restrict__ src, uint16_t* __restrict__ eperm,
+                            int32_t* __restrict__ eadj) {
+  constexpr int EQ = 16 / NSPLIT;              // entries per quarter (host: only for 16 % NSPLIT == 0)
+  constexpr int MQ = kGatherMaxAdj / EQ;       // quarters per chunk, at most
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nchunks;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r0 = row_start[c], r1 = row_start[c + 1];
+    const int64_t a0 = adj_ptr[r0];
+    const int na = (int)(adj_ptr[r1] - a0);
+    if (na <= 0) continue;
+    const int64_t b0 = indptr[r0];
+    const int nq = (na + EQ - 1) / EQ;
+    uint8_t h[MQ][16], fill[MQ];
+    for (int q = 0; q < nq; ++q) {
+      fill[q] = 0;
+      for (int r = 0; r < 16; ++r) h[q][r] = 0;
+    }
+    const int st = gather_perm_stride(na);
+    const float inv = 1.0f / (float)na;
+    for (int jj = 0; jj < na; ++jj) {
+      const int j = gather_perm(jj, na, st, inv);
+      const int64_t e = a0 + j;
+      int64_t lo = r0, hi = r1 - 1;
+      while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (adj_ptr[mid] <= e) lo = mid; else hi = mid - 1;
+      }
+      const int rowlo = (int)(indptr[lo] - b0);
+      uint8_t res[NN];
+      for (int b = 0; b < NN; ++b) res[b] = (uint8_t)((rowlo + src[e * NN + b]) & 15);
+      int best = -1, bc = 1 << 30;
+      for (int q = 0; q < nq; ++q) {
+        const int cap = q + 1 < nq ? EQ : na - EQ * (nq - 1);
+        if (fill[q] >= cap) continue;
+        int cost = 0;
+        for (int b = 0; b < NN; ++b) cost += h[q][res[b]];
+        if (cost < bc) { bc = cost; best = q; }
+      }
+      const int pos = best * EQ + fill[best];
+      ++fill[best];
+      for (int b = 0; b < NN; ++b) ++h[best][res[b]];
+      eperm[a0 + pos] = (uint16_t)j;
+      eadj[a0 + pos] = adj_idx[e];
     }
   }
 }
@@ -2163,13 +2237,14 @@ static int lin_simplex_nsplit(int ct, int p, int nq) {
   return 0;
 }
 
-extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, fa_plan* plan,
-                             void* stream) {
+extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int32_t* eadj,
+                             fa_plan* plan, void* stream) {
   int rc = check_mesh(mesh);
   if (rc) return rc;
   if (!adj || !A || !plan) return fail(FA_E_ARG, "null argument");
   if (!plan->slots) return fail(FA_E_ARG, "fa_plan_order needs the slot map (fa_plan_slots first)");
   plan->slot_order = 0;
+  plan->eadj = nullptr;
   DevTables T;
   if ((rc = get_tables(mesh->cell_type, mesh->degree, -1, &T))) return rc;
   const int ns = lin_simplex_nsplit(mesh->cell_type, mesh->degree, T.nq);
@@ -2185,18 +2260,38 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
     HIP_TRY(hipMallocAsync((void**)&st, 3 * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(st, 0, 3 * sizeof(unsigned long long), s));
   }
-#define ORD(NN_, NS_) k_order_slots<NN_, NS_><<<grid_for(total), 256, 0, s>>>(plan->row_start, A->indptr, adj->ptr, plan->nchunks, groups, sl, st)
+  // positional plan: the plain map is copied aside (the order kernel rewrites by position)
+  const bool posn = eadj != nullptr && 16 % ns == 0;
+  uint16_t *src = nullptr, *eperm = nullptr;
+  const int64_t nent = mesh->ncells * mesh->nn;
+  if (posn) {
+    HIP_TRY(hipMallocAsync((void**)&src, sizeof(uint16_t) * nent * mesh->nn, s));
+    HIP_TRY(hipMallocAsync((void**)&eperm, sizeof(uint16_t) * nent, s));
+    HIP_TRY(hipMemcpyAsync(src, sl, sizeof(uint16_t) * nent * mesh->nn, hipMemcpyDeviceToDevice, s));
+  }
+#define ORD(NN_, NS_)                                                                                         \
+  do {                                                                                                        \
+    if (posn)                                                                                                 \
+      k_plan_perm<NN_, NS_><<<grid_for(plan->nchunks), 64, 0, s>>>(plan->row_start, A->indptr, adj->ptr,      \
+                                                                   adj->idx, plan->nchunks, src, eperm, eadj);   \
+    k_order_slots<NN_, NS_><<<grid_for(total), 256, 0, s>>>(plan->row_start, A->indptr, adj->ptr, plan->nchunks, \
+                                                            groups, sl, src, eperm, st);                      \
+  } while (0)
+  bool ok = true;
   if (mesh->nn == 3 && ns == 1) ORD(3, 1);
   else if (mesh->nn == 6 && ns == 2) ORD(6, 2);
   else if (mesh->nn == 4 && ns == 2) ORD(4, 2);
   else if (mesh->nn == 10 && ns == 2) ORD(10, 2);
   else if (mesh->nn == 10 && ns == 5) ORD(10, 5);
   else if (mesh->nn == 10 && ns == 1) ORD(10, 1);
-  else {
+  else ok = false;
+#undef ORD
+  if (src) HIP_TRY(hipFreeAsync(src, s));
+  if (eperm) HIP_TRY(hipFreeAsync(eperm, s));
+  if (!ok) {
     if (st) (void)hipFreeAsync(st, s);
     return FA_OK;
   }
-#undef ORD
   LAUNCH_CHECK();
   if (st) {
     unsigned long long h[3];
@@ -2208,6 +2303,7 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   }
   HIP_TRY(hipStreamSynchronize(s));
   plan->slot_order = ns;
+  plan->eadj = posn ? eadj : nullptr;
   return FA_OK;
 }
 
@@ -2258,6 +2354,7 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
   plan->max_adj = ma;
   plan->slots = nullptr;
   plan->slot_order = 0;
+  plan->eadj = nullptr;
   return FA_OK;
 }
 
@@ -2374,6 +2471,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   if (P.slot_order && !(MAT == 0 && R::SIMP && NN % NSPLIT == 0 && P.slot_order == NSPLIT)) {
     P.slots = nullptr;
     P.slot_order = 0;
+    P.eadj = nullptr;
   }
   static_assert(NN * GD <= 32, "bc mask holds 32 dofs");
   const int64_t nc = P.M.ncells;
@@ -2442,6 +2540,7 @@ static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc,
   if (P.slot_order) {
     P.slots = nullptr;
     P.slot_order = 0;
+    P.eadj = nullptr;
   }
   if (W.mode == GatherStage::SIZE) {
     *W.bytes = align256((int64_t)sizeof(double) * 9 * NN * NN * nc);
@@ -2576,6 +2675,7 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks;
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
+    P.eadj = P.slot_order ? plan->eadj : nullptr;
     P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr;
     bool handled = false;
     rc = dispatch_gather(mesh, T, F.kind, P, bc, s, &handled);
@@ -2649,6 +2749,7 @@ static int gather_stage(const fa_mesh* mesh, const fa_form* form, const fa_adjac
     P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks;
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
+    P.eadj = P.slot_order ? plan->eadj : nullptr;
   }
   bool handled = false;
   rc = dispatch_gather(mesh, T, F.kind, P, bc, s, &handled, W);

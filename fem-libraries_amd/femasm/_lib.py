@@ -80,6 +80,7 @@ class fa_plan(ctypes.Structure):
         ("slots", ctypes.c_void_p),
         ("slot_order", ctypes.c_int32),
         ("_pad", ctypes.c_int32),
+        ("eadj", ctypes.c_void_p),
     ]
 
 
@@ -95,7 +96,7 @@ SIGNATURES = {
     "fa_sparsity_fill": (ctypes.c_int, [P, P, P, P, P]),
     "fa_plan_gather": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_plan_slots": (ctypes.c_int, [P, P, P, P, P, P]),
-    "fa_plan_order": (ctypes.c_int, [P, P, P, P, P]),
+    "fa_plan_order": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_tabulate_cells": (ctypes.c_int, [P, P, I64, I64, P, P]),
     "fa_assemble_matrix": (ctypes.c_int, [P, P, P, P, P, D, P, I32, P]),
     "fa_gather_work_bytes": (ctypes.c_int, [P, P, P]),

@@ -470,6 +470,23 @@ def _fa_bsr(A: MatrixCSR, part: int = 0) -> _lib.fa_bsr:
     return A._fa_bsr(part)
 
 
+def _plan_order(V, fm, adj, fb, plan, sh, eadj=None):
+    """Bank-conflict-aware LDS order of the affine-simplex gather (fa_plan_order). FEMASM_SLOT_ORDER:
+    "pos" (default) also balances which entries share a 16-lane quarter (positional plan, one int32
+    per adjacency entry), "1" orders each lane's blocks only, "0" keeps the plain slot map."""
+    mode = os.environ.get("FEMASM_SLOT_ORDER", "pos")
+    if mode == "0":
+        return None
+    if mode == "pos" and eadj is None:
+        eadj = torch.empty(V.mesh.num_cells * V.nn, dtype=torch.int32, device=V.mesh.device)
+    if mode != "pos":
+        eadj = None
+    _lib.check(_lib.load().fa_plan_order(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb),
+                                         eadj.data_ptr() if eadj is not None else None, ctypes.byref(plan), sh),
+               "fa_plan_order")
+    return eadj if plan.eadj else None
+
+
 def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0):
     """Row-chunk plan of the gather kernel for one row part of A's pattern (cached on V)."""
     plans = V.__dict__.setdefault("_plans", {})
@@ -484,7 +501,7 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0):
         sh = _lib.stream_handle(V.mesh.device)
         _lib.check(L.fa_plan_gather(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), rs.data_ptr(),
                                     ctypes.byref(plan), sh), "fa_plan_gather")
-        slots = None
+        slots = eadj = None
         mode = os.environ.get("FEMASM_SLOTS", "auto")
         # Per (adjacency entry, column node) block position in its row: no LDS search in the
         # kernel, for 2 B x nn^2 extra reads per cell. Measured with the interleaved-search
@@ -494,11 +511,8 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0):
             slots = torch.empty(V.mesh.num_cells * V.nn * V.nn, dtype=torch.int16, device=V.mesh.device)
             _lib.check(L.fa_plan_slots(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), slots.data_ptr(),
                                        ctypes.byref(plan), sh), "fa_plan_slots")
-            # bank-conflict-aware block order for the affine-simplex kernels (FEMASM_SLOT_ORDER=0: off)
-            if os.environ.get("FEMASM_SLOT_ORDER", "1") != "0":
-                _lib.check(L.fa_plan_order(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), ctypes.byref(plan),
-                                           sh), "fa_plan_order")
-        plans[key] = (plan, rs, A.indptr, slots)
+            eadj = _plan_order(V, fm, adj, fb, plan, sh)
+        plans[key] = (plan, rs, A.indptr, slots, eadj)
     return plans[key][0]
 
 
@@ -580,12 +594,12 @@ class SplitGather:
             for i in live[:1]:
                 _lib.check(L.fa_plan_slots(ctypes.byref(self.fm), ctypes.byref(self.adj), ctypes.byref(self.subs[i]),
                                            self.slots.data_ptr(), ctypes.byref(self.plans[i]), self.sh), "fa_plan_slots")
+            self.eadj = None  # one positional entry buffer: the plans' entries are disjoint
             for i in live:
                 self.plans[i].slots = self.slots.data_ptr()
                 self.plans[i].slot_order = 0
-                if os.environ.get("FEMASM_SLOT_ORDER", "1") != "0":
-                    _lib.check(L.fa_plan_order(ctypes.byref(self.fm), ctypes.byref(self.adj), ctypes.byref(self.subs[i]),
-                                               ctypes.byref(self.plans[i]), self.sh), "fa_plan_order")
+                e = _plan_order(V, self.fm, self.adj, self.subs[i], self.plans[i], self.sh, self.eadj)
+                self.eadj = e if e is not None else self.eadj
 
     def prepare(self):
         _lib.check(self.L.fa_gather_prepare(ctypes.byref(self.fm), ctypes.byref(self.ff), _lib.ptr(self.marker),

@@ -117,6 +117,9 @@ typedef struct {
   int32_t slot_order;        /* 0: `slots` is that plain map; > 0: fa_plan_order rewrote it for the
                                 gather's item order (value = the kernel's column split) */
   int32_t _pad;
+  const int32_t* eadj;       /* positional plan (fa_plan_order with an entry buffer), else NULL:
+                                each chunk's adjacency entries in the plan's bank-balanced order;
+                                `slots` is then indexed by that position, chunk-relative */
 } fa_plan;
 
 const char* fa_last_error(void);
@@ -145,13 +148,19 @@ int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A
 int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, uint16_t* slots, fa_plan* plan,
                   void* stream);
 
-/* Bank-conflict-aware order for the gather's LDS adds (affine simplices, linear elasticity):
- * rewrites plan->slots in place so that, for each group of 32 lanes of the kernel's item
- * mapping, every lane visits its blocks in an order that spreads each step's LDS addresses over
- * the banks; entries then hold (b << 10) | position. Sets plan->slot_order; a no-op (slot_order 0)
- * for elements whose gather does not read an ordered map. Run after fa_plan_slots for EVERY
- * plan sharing the slot map (fa_plan_slots rewrites all rows). */
-int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, fa_plan* plan, void* stream);
+/* Bank-conflict-aware order for the gather's LDS adds (affine simplices, linear elasticity).
+ * Each 16-lane quarter of a wave adds into LDS in passes set by its lanes' slots mod 16
+ * (measured, tools/probe/lds_bank_probe.hip). With eadj == NULL, rewrites plan->slots in place so
+ * that every lane of a quarter of the kernel's fixed item mapping visits its blocks in an order
+ * that spreads each step over the banks; entries hold (b << 10) | position in the row. With eadj
+ * (caller-owned device buffer of ncells*nn int32), the plan also chooses which adjacency entries
+ * share a quarter (balancing their residues), writes each chunk's entries in that order to eadj,
+ * and rewrites plan->slots by position with chunk-relative block positions (plan->eadj = eadj).
+ * Sets plan->slot_order; a no-op (slot_order 0) for elements whose gather does not read an
+ * ordered map. Run after fa_plan_slots for EVERY plan sharing the slot map (fa_plan_slots
+ * rewrites all rows). */
+int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int32_t* eadj, fa_plan* plan,
+                  void* stream);
 
 /* Per-cell element matrices Ae [ncells_out][nn*bs][nn*bs] (dof = node*bs + comp) for cells
  * [c0, c0+ncells_out) — the batched ufcx tabulate_tensor / AssembleElementGrad. */

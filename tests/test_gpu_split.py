@@ -76,19 +76,20 @@ def test_in_kernel_slot_search(dev, oracle, monkeypatch, ct, p, n):
     assert err <= RTOL, err
 
 
-@pytest.mark.parametrize("order", ["1", "0"])
+@pytest.mark.parametrize("order", ["pos", "1", "0"])
 @pytest.mark.parametrize("ct,p,n", [("tetrahedron", 2, 5), ("tetrahedron", 1, 6), ("triangle", 2, 9),
                                     ("triangle", 1, 12)])
 def test_slot_order(dev, oracle, monkeypatch, order, ct, p, n):
-    """fa_plan_order's bank-conflict-aware block order (default) and the plain slot map
-    (FEMASM_SLOT_ORDER=0) both give the oracle's matrix."""
+    """fa_plan_order's positional plan (default), its per-lane block order alone, and the plain slot map
+    (FEMASM_SLOT_ORDER "pos", "1", "0") all give the oracle's matrix."""
     from femasm import fem
 
     monkeypatch.setenv("FEMASM_SLOT_ORDER", order)
     V, a, bcs, indptr, indices, ref = _problem(dev, oracle, ct, p, n)
     A = fem.assemble_matrix(a, bcs=bcs)
     plan = next(iter(V.__dict__["_plans"].values()))[0]
-    assert (plan.slot_order > 0) == (order == "1")
+    assert (plan.slot_order > 0) == (order != "0")
+    assert bool(plan.eadj) == (order == "pos")
     torch.cuda.synchronize()
     err = np.abs(A.data.cpu().numpy() - ref).max() / np.abs(ref).max()
     assert err <= RTOL, err
