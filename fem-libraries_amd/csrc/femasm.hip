@@ -830,15 +830,21 @@ static constexpr int kGatherMaxRows = 128;      // rows per chunk
 // gather variant whose blocks come from a per-cell block store [cell][a][b][GD][GD] (hexahedra:
 // written by the MFMA kernel) instead of being computed from a record
 constexpr int MAT_BLOCKS = 9;
+// linear elasticity with one Poisson ratio for all cells (E per cell): lam / mu = r is uniform, so
+// lam G + mu G^T = mu |J| Ji^T (r Ahat + Ahat^T) Ji; the record holds s Ji with s^2 = mu |J|
+// (and the sign of mu |J|), the table B_ab = r Ahat_ab + Ahat_ab^T, and
+// K = H + tr(H) / (1 + r) I with H = (s Ji)^T B (s Ji): 19 fewer FP64 ops per block
+constexpr int MAT_LINU = 10;
 
 template <int GD, int NV, int NQ, int MAT>
 struct Rec {
   static constexpr bool SIMP = (NV == GD + 1);
   static constexpr int N = GD * GD;
   static constexpr int NTRI = N * (N + 1) / 2;  // stored upper triangle of the tangent
-  // LIN simplex: Ji[GD*GD], wdet, lam, mu | LIN tensor: NQ x (Ji[GD*GD], wdet), lam, mu |
+  // LIN simplex: Ji[GD*GD], wdet, lam, mu | LINU (simplex): s Ji[GD*GD], sign(mu wdet) | LIN tensor: NQ x (Ji[GD*GD], wdet), lam, mu |
   // DAMAGE (P1 tri): g[3][2], w, H[3][3] | NEO (simplex): Ji[GD*GD], wdet, NQ x A_q upper triangle
   static constexpr int RAW = MAT == MAT_BLOCKS ? 2
+                             : MAT == MAT_LINU ? GD * GD + 1
                              : MAT == FA_ASYM_DAMAGE ? 16
                              : MAT == FA_NEO_HOOKEAN ? N + 1 + NQ * NTRI
                                                      : (SIMP ? GD * GD + 3 : NQ * (GD * GD + 1) + 2);
@@ -869,7 +875,8 @@ struct GatherArgs {
   const int8_t* bc;
   double diag;
   const double* tab;  // device tables: wq | dphi | gdphi
-  const double* ahat; // simplex reference tensor [nn][nn][GD][GD]
+  const double* ahat; // simplex reference tensor [nn][nn][GD][GD] (MAT_LINU: the table B)
+  double trc;         // MAT_LINU: 1 / (1 + lam / mu)
   const double* rec;  // [ncells][Rec::SIZE]
   const uint32_t* bcmask;  // [ncells] or NULL
   int* err;
@@ -921,6 +928,18 @@ __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, co
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) r[7 + 3 * i + j] = H[i][j];
+  } else if constexpr (MAT == MAT_LINU) {
+    static_assert(R::SIMP, "uniform-nu records: affine simplices");
+    double lam, mu;
+    cell_lame(F, c, lam, mu);
+    double Ji[GD][GD];
+    const double s2 = mu * fabs(simplex_geometry<GD>(M, c, Ji));
+    const double sc = sqrt(fabs(s2));
+#pragma unroll
+    for (int i = 0; i < GD; ++i)
+#pragma unroll
+      for (int k = 0; k < GD; ++k) r[i * GD + k] = sc * Ji[i][k];
+    r[GD * GD] = s2 < 0.0 ? -1.0 : 1.0;
   } else {
     double lam, mu;
     cell_lame(F, c, lam, mu);
@@ -1063,6 +1082,9 @@ __device__ __forceinline__ void lds_add_block(double* acc, int s, double (&K)[GD
 #endif
 #ifndef FA_GATHER_PERMUTE
 #define FA_GATHER_PERMUTE 1  // measured +16 % on config E at n = 120 (fewer same-slot LDS adds per instruction)
+#endif
+#ifndef FA_GATHER_APIPE
+#define FA_GATHER_APIPE 0  // measured slower: 5 VGPR spills, config E 50.6 -> 55.2 ms
 #endif
 #ifndef FA_GATHER_UNROLL_B
 #define FA_GATHER_UNROLL_B 1
@@ -1281,7 +1303,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   // (neo-Hookean: measured 3 % faster without the permutation, n = 120)
   constexpr bool PERM = FA_GATHER_PERMUTE && !NEO;
   // kernels that can run a positional plan (the ordered-slot affine-simplex elasticity path)
-  constexpr bool POSM = MAT == 0 && SIMP && NN % NSPLIT == 0;
+  constexpr bool POSM = (MAT == 0 || MAT == MAT_LINU) && SIMP && NN % NSPLIT == 0;
   auto perm_stride = [&](int na_) { return PERM ? gather_perm_stride(na_) : 1; };
   auto perm = [&](int jj, int na_, int st, float inv) {
     if constexpr (!PERM) return jj;
@@ -1525,7 +1547,11 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       }
     } else if constexpr (SIMP) {
       // affine simplex: G_ab = |J| Ji^T Ahat_ab Ji  (reference-tensor form)
-      const double wdet = r[BS2], lam = r[BS2 + 1] * wdet, mu = r[BS2 + 2] * wdet;
+      constexpr bool LINU = MAT == MAT_LINU;
+      // LINU: r = s Ji, r[BS2] = sign; LIN: r = Ji, |J|, lam, mu
+      const double wdet = LINU ? 1.0 : r[BS2], lam = LINU ? 0.0 : r[LINU ? 0 : BS2 + 1] * wdet,
+                   mu = LINU ? 0.0 : r[LINU ? 0 : BS2 + 2] * wdet;
+      const bool negw = LINU && __any(r[BS2] < 0.0);  // wave-uniform: a cell with mu |J| < 0
       int sl[NBG];  // slots of the item's column nodes, searched together
       // their local column indices b, 6 bits each (the plan's order when slot_order is set)
       static_assert(NBG * 6 <= 64 && NN <= 64, "packed column list");
@@ -1556,19 +1582,31 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
 #endif
       const uint32_t rowm = (mask >> (aloc * GD)) & ((1u << GD) - 1);
       const double* Ah0 = (FA_GATHER_AHAT_GLOBAL ? P.ahat : s_ahat) + aloc * NN * BS2;
+      // Reference-tensor reads one block ahead: block bb+1's table entry is read before block
+      // bb's adds are issued, so the wait for it (an in-order lgkmcnt) does not also wait for
+      // those nine LDS atomics to complete (FA_GATHER_APIPE=0: read at the top of each block)
+      constexpr bool APIPE = FA_GATHER_APIPE && NN % NSPLIT == 0 && FA_ABL != 4;
+      double Ahn[BS2];
+      int bnext = (int)(bcp & 63);
+      if constexpr (APIPE) {
+#pragma unroll
+        for (int e = 0; e < BS2; ++e) Ahn[e] = Ah0[bnext * BS2 + e];
+      }
 #pragma unroll FA_GATHER_UNROLL_B
       for (int bb = 0; bb < NBG; ++bb) {
         if (NN % NSPLIT != 0 && part * NBG + bb >= NN) break;
-        const int b = (int)(bcp & 63);  // rolled loop: shift the column list like the slot list
+        const int b = APIPE ? bnext : (int)(bcp & 63);  // rolled loop: shift the column list like the slot list
         bcp >>= 6;
-        const double* Ah = Ah0 + b * BS2;
 #if FA_ABL == 4
         double Ahr[BS2];
 #pragma unroll
         for (int e = 0; e < BS2; ++e) Ahr[e] = 0.1 * (e + aloc) + bb;
         const double* Ahp = Ahr;
 #else
-        const double* Ahp = Ah;
+        double Ahc[BS2];
+#pragma unroll
+        for (int e = 0; e < BS2; ++e) Ahc[e] = APIPE ? Ahn[e] : Ah0[b * BS2 + e];
+        const double* Ahp = Ahc;
 #endif
         double T[GD][GD];  // T = Ahat Ji
 #pragma unroll
@@ -1591,7 +1629,32 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
             G[e][d] = g;
           }
         double K[GD][GD];
-        lin_block<GD>(G, lam, mu, K);
+        if constexpr (LINU) {
+          double tr = G[0][0];
+#pragma unroll
+          for (int i = 1; i < GD; ++i) tr += G[i][i];
+          tr *= P.trc;
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int k = 0; k < GD; ++k) K[i][k] = i == k ? G[i][k] + tr : G[i][k];
+          if (negw) {
+            const double sg = r[BS2];
+#pragma unroll
+            for (int i = 0; i < GD; ++i)
+#pragma unroll
+              for (int k = 0; k < GD; ++k) K[i][k] *= sg;
+          }
+        } else {
+          lin_block<GD>(G, lam, mu, K);
+        }
+        if constexpr (APIPE) {
+          if (bb + 1 < NBG) {
+            bnext = (int)(bcp & 63);
+#pragma unroll
+            for (int e = 0; e < BS2; ++e) Ahn[e] = Ah0[bnext * BS2 + e];
+          }
+        }
         int s = sl[0];  // rolled loop: shift the slot list instead of indexing it
 #pragma unroll
         for (int k = 0; k + 1 < NBG; ++k) sl[k] = sl[k + 1];
@@ -2463,12 +2526,22 @@ struct GatherStage {
 };
 static inline int64_t align256(int64_t b) { return (b + 255) & ~int64_t(255); }
 
+template <int GD>
+__global__ void k_bhat(const double* __restrict__ ahat, int nblk, double r, double* __restrict__ bhat) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nblk; t += gridDim.x * blockDim.x)
+#pragma unroll
+    for (int i = 0; i < GD; ++i)
+#pragma unroll
+      for (int k = 0; k < GD; ++k)
+        bhat[t * GD * GD + i * GD + k] = r * ahat[t * GD * GD + i * GD + k] + ahat[t * GD * GD + k * GD + i];
+}
+
 template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT>
 static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const GatherStage& W) {
   using R = Rec<GD, NV, NQ, MAT>;
   // ordered (packed) slots are read only by the affine-simplex linear kernel of the same NSPLIT;
   // any other kernel searches its slots in LDS instead
-  if (P.slot_order && !(MAT == 0 && R::SIMP && NN % NSPLIT == 0 && P.slot_order == NSPLIT)) {
+  if (P.slot_order && !((MAT == 0 || MAT == MAT_LINU) && R::SIMP && NN % NSPLIT == 0 && P.slot_order == NSPLIT)) {
     P.slots = nullptr;
     P.slot_order = 0;
     P.eadj = nullptr;
@@ -2500,6 +2573,15 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     int64_t* desc = nullptr;
     if ((rc = chunk_desc(P, &desc, s))) return rc;
     const int64_t grid = gather_grid(k_gather<GD, NN, NV, NQ, NSPLIT, MAT>, P.nchunks);
+    double* bhat = nullptr;
+    if constexpr (MAT == MAT_LINU) {  // B_ab = r Ahat_ab + Ahat_ab^T for this form's nu
+      const double nu = P.F.nu, rr = 2.0 * nu / (1.0 - 2.0 * nu);
+      if ((rc = scratch_alloc((void**)&bhat, sizeof(double) * NN * NN * GD * GD, s))) return rc;
+      k_bhat<GD><<<grid_for(NN * NN), 256, 0, s>>>(P.ahat, NN * NN, rr, bhat);
+      LAUNCH_CHECK();
+      P.ahat = bhat;
+      P.trc = 1.0 / (1.0 + rr);
+    }
 #if FA_GATHER_TIMING
     {
       unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -2521,6 +2603,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     }
 #endif
     HIP_TRY(hipFreeAsync(desc, s));
+    if (bhat) HIP_TRY(hipFreeAsync(bhat, s));
   }
   if (W.mode == GatherStage::FULL) {
     HIP_TRY(hipFreeAsync(rec, s));
@@ -2574,6 +2657,14 @@ static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc,
   return FA_OK;
 }
 
+// the uniform-nu affine-simplex kernels (MAT_LINU): E per cell with one nu, away from nu = 1/2
+// (FEMASM_LINU=0: the general lam / mu kernel, a measurement knob)
+static bool lin_uniform_nu(const FormView& F) {
+  const char* e = getenv("FEMASM_LINU");
+  if (e && e[0] == '0') return false;
+  return F.kind == FA_LINEAR_ELASTICITY && F.E && F.nu > -0.99 && F.nu < 0.49;
+}
+
 static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const GatherArgs& P, const int8_t* bc,
                            hipStream_t s, bool* handled, const GatherStage& W = GatherStage()) {
   *handled = true;
@@ -2591,6 +2682,13 @@ static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const
     if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, FA_NEO_HOOKEAN>(P, bc, s, W);
     *handled = false;
     return FA_OK;
+  }
+  if (lin_uniform_nu(P.F)) {
+    if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, MAT_LINU>(P, bc, s, W);
+    if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, MAT_LINU>(P, bc, s, W);
+    if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, MAT_LINU>(P, bc, s, W);
+    if (ct == FA_TETRAHEDRON && p == 2 && nq == 4)
+      return launch_gather<3, 10, 4, 4, FA_P2TET_NSPLIT, MAT_LINU>(P, bc, s, W);
   }
   if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, 0>(P, bc, s, W);
   if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, 0>(P, bc, s, W);
