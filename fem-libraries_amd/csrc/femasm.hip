@@ -1083,6 +1083,9 @@ __device__ __forceinline__ void lds_add_block(double* acc, int s, double (&K)[GD
 #ifndef FA_GATHER_PERMUTE
 #define FA_GATHER_PERMUTE 1  // measured +16 % on config E at n = 120 (fewer same-slot LDS adds per instruction)
 #endif
+#ifndef FA_GATHER_SU
+#define FA_GATHER_SU 4  // 16-B values per thread per store batch (LDS reads issued together)
+#endif
 #ifndef FA_GATHER_APIPE
 #define FA_GATHER_APIPE 0  // measured slower: 5 VGPR spills, config E 50.6 -> 55.2 ms
 #endif
@@ -1330,7 +1333,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   __syncthreads();
   int kpar = 0;
 #if FA_GATHER_TIMING
-  unsigned long long gt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long gt[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long gt_top = __builtin_amdgcn_s_memtime();
 #endif
   for (;;) {
@@ -1804,6 +1807,10 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     if (!PIPE) fetch(nxt);
     stage_meta(nxt);
   }
+#if FA_GATHER_TIMING
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  gt[9] += __builtin_amdgcn_s_memtime() - gt_c;
+#endif
   // Stream the chunk out: 16-B non-temporal stores (the matrix is written once and not re-read
   // by this launch, so it should not evict the records and dofmap the next chunks share).
   {
@@ -1821,7 +1828,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     dv2* out2 = reinterpret_cast<dv2*>(out + h);
     // a batch's LDS reads are issued together, then its stores (one LDS latency per batch,
     // not per store: the LDS is busy with other workgroups' atomics)
-    constexpr int SU = 4;
+    constexpr int SU = FA_GATHER_SU;
     for (int t0 = tid; t0 < np; t0 += 256 * SU) {
       dv2 v[SU];
 #pragma unroll
@@ -1872,7 +1879,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   }
 #if FA_GATHER_TIMING
   if ((tid & 63) == 0)
-    for (int k = 0; k < 9; ++k) atomicAdd(&g_gather_timing[k], gt[k]);
+    for (int k = 0; k < 10; ++k) atomicAdd(&g_gather_timing[k], gt[k]);
 #endif
 }
 
@@ -2189,24 +2196,44 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
     for (int t = 0; t < NBG; ++t) ident += step_max(t);
     for (int r = 0; r < 16; ++r) dmax = max(dmax, deg[r]);
     lb = max(lb, dmax);
-    for (int pass = 0; pass < 64; ++pass) {
+    // step maxima and how many residues reach them: a swap is then priced in O(1) and the two
+    // steps are recounted only when it is taken
+    int mx[NBG], nmx[NBG];
+    auto recount = [&](int t) {
+      int m = 0, n = 0;
+      for (int r = 0; r < 16; ++r) {
+        const int v = cnt[t][r];
+        if (v > m) { m = v; n = 1; } else if (v == m) ++n;
+      }
+      mx[t] = m;
+      nmx[t] = n;
+    };
+    // new maximum of step t after one add moves from residue ro (count co) to rn (count cn)
+    auto moved_max = [&](int t, int co, int cn) {
+      if (cn + 1 > mx[t]) return cn + 1;
+      if (co == mx[t] && nmx[t] == 1 && cn + 1 < mx[t]) return mx[t] - 1;
+      return mx[t];
+    };
+    for (int t = 0; t < NBG; ++t) recount(t);
+    for (int pass = 0; pass < 32; ++pass) {
       bool improved = false;
       for (int q = 0; q < nl; ++q)
         for (int t1 = 0; t1 < NBG; ++t1)
           for (int t2 = t1 + 1; t2 < NBG; ++t2) {
             const int ra = res[q][pick[q][t1]], rb = res[q][pick[q][t2]];
             if (ra == rb) continue;
-            const int m1 = step_max(t1), m2 = step_max(t2);
-            const int sq = 2 * (cnt[t1][rb] - cnt[t1][ra]) + 2 + 2 * (cnt[t2][ra] - cnt[t2][rb]) + 2;
-            --cnt[t1][ra]; ++cnt[t1][rb]; --cnt[t2][rb]; ++cnt[t2][ra];
-            const int d = step_max(t1) + step_max(t2) - m1 - m2;
+            const int a1 = cnt[t1][ra], b1 = cnt[t1][rb], a2 = cnt[t2][ra], b2 = cnt[t2][rb];
+            // step t1: ra -> rb; step t2: rb -> ra
+            const int d = moved_max(t1, a1, b1) + moved_max(t2, b2, a2) - mx[t1] - mx[t2];
+            const int sq = 2 * (b1 - a1) + 2 + 2 * (a2 - b2) + 2;
             if (d < 0 || (d == 0 && sq < 0)) {
+              --cnt[t1][ra]; ++cnt[t1][rb]; --cnt[t2][rb]; ++cnt[t2][ra];
               const uint8_t x = pick[q][t1];
               pick[q][t1] = pick[q][t2];
               pick[q][t2] = x;
+              recount(t1);
+              recount(t2);
               improved = true;
-            } else {
-              ++cnt[t1][ra]; --cnt[t1][rb]; ++cnt[t2][rb]; --cnt[t2][ra];
             }
           }
       if (!improved) break;
@@ -2598,8 +2625,8 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       const double n = (double)(t[6] ? t[6] : 1);
       fprintf(stderr, "[gather timing] per wave-chunk (shader clocks): items %.0f | wait-items %.0f | store %.0f | "
                       "wait-store %.0f | stage %.0f | wait-stage %.0f | wave-chunks %llu | item loads %.0f | "
-                      "item blocks %.0f\n",
-              t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5] / n, t[6], t[7] / n, t[8] / n);
+                      "item blocks %.0f | store: meta staging %.0f\n",
+              t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5] / n, t[6], t[7] / n, t[8] / n, t[9] / n);
     }
 #endif
     HIP_TRY(hipFreeAsync(desc, s));

@@ -1,12 +1,13 @@
 #!/bin/bash
 # Build compile-time variants of libfemasm into abl/ and bench each with FEMASM_LIB.
+# (SKIP_BUILD=1: use the abl/ libraries built beforehand, e.g. in the CPU container)
 # usage: VARIANTS="name:-DFLAG=1 -DX=2;name2:" CFG=E NARG="--n 120" bash tools/variants.sh
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out abl
 IFS=';' read -ra VS <<< "$VARIANTS"
 cd fem-libraries_amd/csrc
-for v in "${VS[@]}"; do
+[ -n "$SKIP_BUILD" ] || for v in "${VS[@]}"; do
   name=${v%%:*}; flags=${v#*:}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -munsafe-fp-atomics $flags \
     -o ../../abl/libfemasm_$name.so femasm.hip &
