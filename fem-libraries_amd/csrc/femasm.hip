@@ -1083,6 +1083,22 @@ __device__ __forceinline__ void lds_add_block(double* acc, int s, double (&K)[GD
 #ifndef FA_GATHER_PERMUTE
 #define FA_GATHER_PERMUTE 1  // measured +16 % on config E at n = 120 (fewer same-slot LDS adds per instruction)
 #endif
+#ifndef FA_GATHER_STORE
+#define FA_GATHER_STORE 0  // chunk stores: 0 non-temporal, 1 plain, 2 sc1 (write-through)
+#endif
+template <typename T>
+__device__ __forceinline__ void out_store(const T& v, T* p) {
+  if constexpr (FA_GATHER_STORE == 0) {
+    __builtin_nontemporal_store(v, p);
+  } else if constexpr (FA_GATHER_STORE == 1) {
+    *p = v;
+  } else {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+#ifndef FA_GATHER_BATCH
+#define FA_GATHER_BATCH 2  // chunks per chunk-counter atomic: measured 1 50.7, 2 48.2, 8 48.2 ms (E); C 1.95 / 1.95 / 2.02
+#endif
 #ifndef FA_GATHER_SU
 #define FA_GATHER_SU 4  // 16-B values per thread per store batch (LDS reads issued together)
 #endif
@@ -1176,15 +1192,30 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   // the next one), three chunks ahead so the atomic's latency hides behind a chunk's work; the
   // index reaches the other lanes through LDS.
   __shared__ int64_t s_idx[3];
+  // lane 0 takes FA_GATHER_BATCH consecutive chunks per counter atomic and serves them from this
+  // batch [s_bat[0], s_bat[1]): the same-address atomics of an XCD's 128 workgroups on one L2
+  // line were the kernel's throughput limit (one per ~80 ns per counter at one chunk per atomic)
+  __shared__ int64_t s_bat[2];
   uint32_t qdone = 0u;  // lane 0: ranges found exhausted
+  auto take_batch = [&](int q, unsigned long long c) {
+    if ((int64_t)c < per) {
+      const int64_t base = q * per + (int64_t)c;
+      const int64_t end = min(q * per + min((int64_t)c + FA_GATHER_BATCH, per), P.nchunks);
+      if (base < end) {
+        s_bat[0] = base;
+        s_bat[1] = end;
+        return;
+      }
+    }
+    qdone |= 1u << q;
+  };
   auto grab = [&]() -> int64_t {
-    for (int t = 0; t < 8; ++t) {
+    for (int t = 0; t < 9; ++t) {
+      if (s_bat[0] < s_bat[1]) return s_bat[0]++;
+      if (t == 8) break;
       const int q = (int)((blockIdx.x + t) & 7);
       if ((qdone >> q) & 1u) continue;
-      const unsigned long long c = atomicAdd(P.ctr + q, 1ull);
-      const int64_t ch = q * per + (int64_t)c;
-      if ((int64_t)c < per && ch < P.nchunks) return ch;
-      qdone |= 1u << q;
+      take_batch(q, atomicAdd(P.ctr + q, (unsigned long long)FA_GATHER_BATCH));
     }
     return P.nchunks;
   };
@@ -1192,6 +1223,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   int64_t idx0, idx1, idx2;
   if (P.ctr) {
     if (tid == 0) {
+      s_bat[0] = s_bat[1] = 0;
       s_idx[0] = grab();
       s_idx[1] = grab();
       s_idx[2] = grab();
@@ -1341,12 +1373,12 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   // wait for its return (a vmcnt wait) does not head the chunk
   unsigned long long gcand = 0ull;
   int gq = -1;
-  if (P.ctr && tid == 0 && nnchunk < P.nchunks) {
+  if (P.ctr && tid == 0 && nnchunk < P.nchunks && s_bat[0] >= s_bat[1]) {  // batch used up
     for (int t = 0; t < 8; ++t) {
       const int q = (int)((blockIdx.x + t) & 7);
       if (!((qdone >> q) & 1u)) { gq = q; break; }
     }
-    if (gq >= 0) gcand = atomicAdd(P.ctr + gq, 1ull);
+    if (gq >= 0) gcand = atomicAdd(P.ctr + gq, (unsigned long long)FA_GATHER_BATCH);
   }
 
   if (PIPE && nchunk < P.nchunks) fetch(nxt);  // lands while this chunk is assembled
@@ -1598,6 +1630,9 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
 #pragma unroll FA_GATHER_UNROLL_B
       for (int bb = 0; bb < NBG; ++bb) {
         if (NN % NSPLIT != 0 && part * NBG + bb >= NN) break;
+#if FA_ABL == 10
+        if (bb >= 1) break;  // timing only: one block per item
+#endif
         const int b = APIPE ? bnext : (int)(bcp & 63);  // rolled loop: shift the column list like the slot list
         bcp >>= 6;
 #if FA_ABL == 4
@@ -1780,12 +1815,9 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   nn2 = nnchunk < P.nchunks ? load_desc(nnchunk) : nxt;
   if (P.ctr && tid == 0) {
     int64_t ch = P.nchunks;
-    if (gq >= 0) {
-      ch = gq * per + (int64_t)gcand;
-      if (!((int64_t)gcand < per && ch < P.nchunks)) {
-        qdone |= 1u << gq;
-        ch = grab();
-      }
+    if (nnchunk < P.nchunks) {  // once the sequence has ended it stays ended
+      if (gq >= 0) take_batch(gq, gcand);
+      ch = grab();
     }
     s_idx[kpar] = ch;
   }
@@ -1822,7 +1854,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     if (acc[tid] == 1.2345e-300) out[tid] = 0.0;  // timing only: no chunk store
     if (false) {
 #endif
-    if (h && tid == 0) __builtin_nontemporal_store(acc[0], out);
+    if (h && tid == 0) out_store(acc[0], out);
     const int np = (nv - h) >> 1;
     typedef double dv2 __attribute__((ext_vector_type(2)));
     dv2* out2 = reinterpret_cast<dv2*>(out + h);
@@ -1842,10 +1874,10 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
 #pragma unroll
       for (int u = 0; u < SU; ++u) {
         const int t = t0 + 256 * u;
-        if (t < np) __builtin_nontemporal_store(v[u], out2 + t);
+        if (t < np) out_store(v[u], out2 + t);
       }
     }
-    if (((nv - h) & 1) && tid == 0) __builtin_nontemporal_store(acc[nv - 1], out + nv - 1);
+    if (((nv - h) & 1) && tid == 0) out_store(acc[nv - 1], out + nv - 1);
 #if FA_ABL == 8
     }
 #endif
