@@ -1096,6 +1096,12 @@ __device__ __forceinline__ void out_store(const T& v, T* p) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
+#ifndef FA_ORDER_KICKS
+// perturbation rounds of the plan's bank-order search (FEMASM_ORDER_KICKS at run time). Config E:
+// 0 -> LDS passes 0.648 of unordered, gather 48.5 ms, plan 3 s; 16 -> 0.568, 48.0 ms, 21 s;
+// 64 -> 0.533, 47.6 ms, 79 s
+#define FA_ORDER_KICKS 16
+#endif
 #ifndef FA_GATHER_BATCH
 #define FA_GATHER_BATCH 2  // chunks per chunk-counter atomic: measured 1 50.7, 2 48.2, 8 48.2 ms (E); C 1.95 / 1.95 / 2.02
 #endif
@@ -2170,7 +2176,7 @@ template <int NN, int NSPLIT>
 __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64_t* __restrict__ indptr,
                               const int64_t* __restrict__ adj_ptr, int64_t nchunks, int groups_per_chunk,
                               uint16_t* __restrict__ slots, const uint16_t* __restrict__ src,
-                              const uint16_t* __restrict__ eperm, unsigned long long* __restrict__ stats) {
+                              const uint16_t* __restrict__ eperm, unsigned long long* __restrict__ stats, int kicks) {
   constexpr int NBG = NN / NSPLIT, Q = 16;
   const int64_t total = nchunks * groups_per_chunk;
   for (int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gid < total;
@@ -2247,28 +2253,69 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
       return mx[t];
     };
     for (int t = 0; t < NBG; ++t) recount(t);
-    for (int pass = 0; pass < 32; ++pass) {
-      bool improved = false;
-      for (int q = 0; q < nl; ++q)
-        for (int t1 = 0; t1 < NBG; ++t1)
-          for (int t2 = t1 + 1; t2 < NBG; ++t2) {
-            const int ra = res[q][pick[q][t1]], rb = res[q][pick[q][t2]];
-            if (ra == rb) continue;
-            const int a1 = cnt[t1][ra], b1 = cnt[t1][rb], a2 = cnt[t2][ra], b2 = cnt[t2][rb];
-            // step t1: ra -> rb; step t2: rb -> ra
-            const int d = moved_max(t1, a1, b1) + moved_max(t2, b2, a2) - mx[t1] - mx[t2];
-            const int sq = 2 * (b1 - a1) + 2 + 2 * (a2 - b2) + 2;
-            if (d < 0 || (d == 0 && sq < 0)) {
-              --cnt[t1][ra]; ++cnt[t1][rb]; --cnt[t2][rb]; ++cnt[t2][ra];
-              const uint8_t x = pick[q][t1];
-              pick[q][t1] = pick[q][t2];
-              pick[q][t2] = x;
-              recount(t1);
-              recount(t2);
-              improved = true;
+    auto swap_pick = [&](int q, int t1, int t2) {
+      const int ra = res[q][pick[q][t1]], rb = res[q][pick[q][t2]];
+      --cnt[t1][ra]; ++cnt[t1][rb]; --cnt[t2][rb]; ++cnt[t2][ra];
+      const uint8_t x = pick[q][t1];
+      pick[q][t1] = pick[q][t2];
+      pick[q][t2] = x;
+      recount(t1);
+      recount(t2);
+    };
+    auto descend = [&]() {
+      for (int pass = 0; pass < 32; ++pass) {
+        bool improved = false;
+        for (int q = 0; q < nl; ++q)
+          for (int t1 = 0; t1 < NBG; ++t1)
+            for (int t2 = t1 + 1; t2 < NBG; ++t2) {
+              const int ra = res[q][pick[q][t1]], rb = res[q][pick[q][t2]];
+              if (ra == rb) continue;
+              const int a1 = cnt[t1][ra], b1 = cnt[t1][rb], a2 = cnt[t2][ra], b2 = cnt[t2][rb];
+              // step t1: ra -> rb; step t2: rb -> ra
+              const int d = moved_max(t1, a1, b1) + moved_max(t2, b2, a2) - mx[t1] - mx[t2];
+              const int sq = 2 * (b1 - a1) + 2 + 2 * (a2 - b2) + 2;
+              if (d < 0 || (d == 0 && sq < 0)) {
+                swap_pick(q, t1, t2);
+                improved = true;
+              }
             }
+        if (!improved) break;
+      }
+    };
+    auto total = [&]() {
+      int c = 0;
+      for (int t = 0; t < NBG; ++t) c += mx[t];
+      return c;
+    };
+    descend();
+    // iterated local search: random pairs of swaps, descend again, keep the best order
+    int best = total();
+    uint8_t bestp[Q][NBG];
+    for (int q = 0; q < nl; ++q)
+      for (int t = 0; t < NBG; ++t) bestp[q][t] = pick[q][t];
+    uint32_t rng = 2654435761u * (uint32_t)(gid + 1);
+    for (int k = 0; k < kicks && best > lb; ++k) {
+      for (int j = 0; j < 2; ++j) {
+        rng ^= rng << 13; rng ^= rng >> 17; rng ^= rng << 5;
+        const int q = (int)(rng % (uint32_t)nl), t1 = (int)((rng >> 8) % NBG), t2 = (int)((rng >> 16) % NBG);
+        if (t1 != t2) swap_pick(q, t1, t2);
+      }
+      descend();
+      const int c = total();
+      if (c <= best) {
+        best = c;
+        for (int q = 0; q < nl; ++q)
+          for (int t = 0; t < NBG; ++t) bestp[q][t] = pick[q][t];
+      } else {  // back to the best order
+        for (int t = 0; t < NBG; ++t)
+          for (int r = 0; r < 16; ++r) cnt[t][r] = 0;
+        for (int q = 0; q < nl; ++q)
+          for (int t = 0; t < NBG; ++t) {
+            pick[q][t] = bestp[q][t];
+            ++cnt[t][res[q][pick[q][t]]];
           }
-      if (!improved) break;
+        for (int t = 0; t < NBG; ++t) recount(t);
+      }
     }
     if (stats) {
       int cost = 0;
@@ -2382,6 +2429,8 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
     HIP_TRY(hipMallocAsync((void**)&st, 3 * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(st, 0, 3 * sizeof(unsigned long long), s));
   }
+  const char* ke = getenv("FEMASM_ORDER_KICKS");
+  const int kicks = ke ? atoi(ke) : FA_ORDER_KICKS;
   // positional plan: the plain map is copied aside (the order kernel rewrites by position)
   const bool posn = eadj != nullptr && 16 % ns == 0;
   uint16_t *src = nullptr, *eperm = nullptr;
@@ -2397,7 +2446,7 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
       k_plan_perm<NN_, NS_><<<grid_for(plan->nchunks), 64, 0, s>>>(plan->row_start, A->indptr, adj->ptr,      \
                                                                    adj->idx, plan->nchunks, src, eperm, eadj);   \
     k_order_slots<NN_, NS_><<<grid_for(total), 256, 0, s>>>(plan->row_start, A->indptr, adj->ptr, plan->nchunks, \
-                                                            groups, sl, src, eperm, st);                      \
+                                                            groups, sl, src, eperm, st, kicks);               \
   } while (0)
   bool ok = true;
   if (mesh->nn == 3 && ns == 1) ORD(3, 1);
