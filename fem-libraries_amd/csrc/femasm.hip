@@ -1099,8 +1099,9 @@ __device__ __forceinline__ void out_store(const T& v, T* p) {
 #ifndef FA_ORDER_KICKS
 // perturbation rounds of the plan's bank-order search (FEMASM_ORDER_KICKS at run time). Config E:
 // 0 -> LDS passes 0.648 of unordered, gather 48.5 ms, plan 3 s; 16 -> 0.568, 48.0 ms, 21 s;
-// 64 -> 0.533, 47.6 ms, 79 s
-#define FA_ORDER_KICKS 16
+// 64 -> 0.533, 47.6 ms, 79 s. Default 0: 16 rounds cost ~18 s of setup for ~0.5 ms per assembly,
+// which a Newton solve (7 assemblies, doc.tex:2051) never earns back
+#define FA_ORDER_KICKS 0
 #endif
 #ifndef FA_GATHER_BATCH
 #define FA_GATHER_BATCH 2  // chunks per chunk-counter atomic: measured 1 50.7, 2 48.2, 8 48.2 ms (E); C 1.95 / 1.95 / 2.02
@@ -1162,6 +1163,8 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   using R = Rec<GD, NV, NQ, MAT>;
   constexpr int BS2 = GD * GD;
   constexpr int MAXB = kGatherLdsValues / (8 * BS2);
+  // ordered slots pack (b << 10) | chunk-relative position: positions must stay below 1024
+  static_assert(MAXB < 1024, "FA_GATHER_LDS too large for the packed ordered-slot map");
   constexpr bool SIMP = R::SIMP;
   constexpr int NBG = (NN + NSPLIT - 1) / NSPLIT;  // column nodes per item
   __shared__ double acc[(MAXB + 1) * BS2];  // + one sink slot for (erroneous) missing columns
@@ -2418,6 +2421,9 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   if ((rc = get_tables(mesh->cell_type, mesh->degree, -1, &T))) return rc;
   const int ns = lin_simplex_nsplit(mesh->cell_type, mesh->degree, T.nq);
   if (ns == 0 || plan->nchunks <= 0) return FA_OK;  // no kernel reads an ordered map: keep plain slots
+  // ordered entries pack (b << 10) | chunk-relative position (k_order_slots): keep the plain map
+  // for a plan whose chunks could hold 1024 blocks or more
+  if (plan->max_blocks >= 1024 || kGatherLdsValues / (8 * mesh->gdim * mesh->gdim) >= 1024) return FA_OK;
   const int groups = (kGatherMaxAdj * ns + 15) / 16;
   hipStream_t s = (hipStream_t)stream;
   const int64_t total = plan->nchunks * groups;

@@ -1,9 +1,11 @@
-"""Full-size parity (BASELINE.json configs at their real sizes): sampled rows of the GPU matrix
-against the CPU oracle assembling exactly the cells adjacent to those rows (so the sampled rows
-are complete), plus size-independent properties. Config E on one GPU allocates ~170 GB."""
-import numpy as np
+"""Full-size parity of the headline workload (config E's mesh, linear-elasticity J): sampled rows
+of the GPU matrix against the CPU oracle assembling exactly the cells adjacent to those rows (so
+the sampled rows are complete), per-row 1e-12 bar (tests/rowparity.py), plus size-independent
+properties. Config E on one GPU allocates ~170 GB. The other configs: tests/test_gpu_configs.py."""
 import pytest
 import torch
+
+from rowparity import sampled_row_parity
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-12
@@ -14,46 +16,6 @@ def dev():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda", 0)
-
-
-def sampled_row_parity(oracle, V, a, A, marker, nsample=2000, seed=0):
-    """Max relative error over `nsample` random rows (relative to the global max |A| of the sample)."""
-    m = V.mesh
-    g = torch.Generator(device="cpu").manual_seed(seed)
-    rows = torch.randint(0, V.num_nodes, (nsample,), generator=g).unique()
-    ptr, idx = V.adjacency()
-    ptr_h = ptr.cpu()
-    segs = [idx[int(ptr_h[r]):int(ptr_h[r + 1])] for r in rows.tolist()]
-    cells = torch.unique(torch.cat(segs).to(torch.int64) // V.nn)
-    sub_nodes_glob = V.dofmap[cells].to(torch.int64)
-    uniq, inv = torch.unique(sub_nodes_glob.reshape(-1), return_inverse=True)
-    sub_cells = inv.reshape(sub_nodes_glob.shape).to(torch.int32).cpu().numpy()
-    sub_geom_glob = m.cells[cells].to(torch.int64)
-    vuniq, vinv = torch.unique(sub_geom_glob.reshape(-1), return_inverse=True)
-    sub_geom = vinv.reshape(sub_geom_glob.shape).to(torch.int32).cpu().numpy()
-    sub_x = m.x[vuniq].cpu().numpy()
-    E = a.E[cells].cpu().numpy()
-    lam, mu = oracle.lame(E, a.nu)
-    bs = V.bs
-    bc = None
-    if marker is not None:
-        dofs = (uniq[:, None] * bs + torch.arange(bs, device=uniq.device)[None, :]).reshape(-1)
-        bc = marker[dofs].cpu().numpy()
-    uniq_h = uniq.cpu().numpy()
-    ip, ix = oracle.sparsity(sub_cells, len(uniq_h))
-    vals = oracle.assemble_elasticity(int(m.cell_type), V.degree, sub_cells, sub_geom, sub_x, lam, mu, ip, ix, bc=bc,
-                                      diag=1.0, qdeg=a.qdeg)
-    loc = {int(gn): k for k, gn in enumerate(uniq_h)}
-    gcols, gvals = A.row_blocks(rows.tolist())
-    scale, err = 0.0, 0.0
-    for r, gc, gv in zip(rows.tolist(), gcols, gvals):
-        lr = loc[r]
-        oc = uniq_h[ix[ip[lr]:ip[lr + 1]]]
-        ov = vals[ip[lr]:ip[lr + 1]]
-        assert np.array_equal(gc, oc), f"row {r}: pattern mismatch"
-        scale = max(scale, float(np.abs(ov).max()))
-        err = max(err, float(np.abs(gv - ov).max()))
-    return err / scale, len(rows)
 
 
 @pytest.mark.parametrize("n", [203])

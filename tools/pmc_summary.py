@@ -45,7 +45,13 @@ def traffic_record(root, kernels=("k_gather", "k_cell_records")):
 if len(sys.argv) > 3:  # pmc_summary.py ROOT KEY OUT_JSON: record traffic for bench.py
     import json
 
+    import hashlib
+
     key, out = sys.argv[2], sys.argv[3]
+    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "fem-libraries_amd", "csrc", "femasm.hip")
+    khash = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
     data = json.load(open(out)) if os.path.exists(out) else {}
-    data[key] = {"bytes": traffic_record(root), "source": f"rocprofv3 --pmc passes in {root} (tools/prof_passes.sh)"}
+    # keyed on the kernel source hash: bench.py refuses a record of another build of femasm.hip
+    data[key] = {"bytes": traffic_record(root), "kernel_hash": khash,
+                 "source": f"rocprofv3 --pmc passes in {root} (tools/prof_passes.sh)"}
     json.dump(data, open(out, "w"), indent=1)
