@@ -877,6 +877,7 @@ struct GatherArgs {
   const double* tab;  // device tables: wq | dphi | gdphi
   const double* ahat; // simplex reference tensor [nn][nn][GD][GD] (MAT_LINU: the table B)
   double trc;         // MAT_LINU: 1 / (1 + lam / mu)
+  double rlm;         // MAT_LINU: lam / mu
   const double* rec;  // [ncells][Rec::SIZE]
   const uint32_t* bcmask;  // [ncells] or NULL
   int* err;
@@ -1075,6 +1076,134 @@ __device__ __forceinline__ void lds_add_block(double* acc, int s, double (&K)[GD
     for (int jj = 0; jj < GD; ++jj) atomicAdd(&acc[s * (GD * GD) + i * GD + jj], K[i][jj]);
 }
 
+// ------------------------------------------------------------------------------------ barycentric blocks
+// Affine P1 / P2 simplex blocks without a reference-tensor table (FA_GATHER_BARY). With barycentric
+// coordinates lambda_0..lambda_d and their (scaled, physical) gradients g_k, every basis gradient is
+// grad phi_b = sum_l c_bl(lambda) g_l with c linear in lambda: vertex b = i: c_bi = 4 lambda_i - 1;
+// edge b = (i, j): c_bi = 4 lambda_j, c_bj = 4 lambda_i (P1: c_bb = 1). The exact integrals
+// int c_ak c_bl / |T| = B (1 + [x_ak = x_bl]) + C(type a, type b), x = the lambda in c, give
+//   G_ab = int grad phi_a grad phi_b^T = |T| [ (B + C) sigma_a sigma_b^T + B sum_x tau_a(x) tau_b(x)^T ]
+// with sigma_a = sum of a's gradients and tau_a(x) the gradient whose coefficient is in lambda_x.
+// B = 16 / ((d+1)(d+2)); C = 1 - 8/(d+1) (vertex-vertex), -4/(d+1) (vertex-edge), 0 (edge-edge).
+// The P2 integrand is quadratic, so this equals the default (exact) quadrature rule up to rounding.
+// The row node a is per item (selected from registers once), the item's columns are compile-time
+// (a static split of the cell's nodes), so a block is ~30 FP64 operations and no LDS table read.
+template <int GD, int NN>
+struct Bary {
+  static constexpr int NV = GD + 1;
+  static constexpr bool P2 = NN > NV;
+  static constexpr int NPART = (GD == 2 && !P2) ? 1 : 2;
+  static constexpr int NB = NN / NPART;
+  // static columns of each part: P2 tet {v0 v1 e(2,3) e(1,3) e(1,2)} {v2 v3 e(0,3) e(0,2) e(0,1)}
+  __host__ __device__ static constexpr int col(int part, int bb) {
+    if (GD == 3 && P2) return part == 0 ? (bb < 2 ? bb : 2 + bb) : (bb < 2 ? 2 + bb : 5 + bb);
+    if (GD == 2 && P2) return part == 0 ? (bb < 2 ? bb : 3) : (bb == 0 ? 2 : 3 + bb);
+    return part * NB + bb;  // P1: vertices in order
+  }
+  // barycentric pair (p, q) of local node b (p = q for a vertex); basix edge order
+  __host__ __device__ static constexpr int ep(int b) {
+    return b < NV ? b : (GD == 3 ? (int)((0x000112u >> (4 * (b - 4))) & 15u) : (int)((0x001u >> (4 * (b - 3))) & 15u));
+  }
+  __host__ __device__ static constexpr int eq(int b) {
+    return b < NV ? b : (GD == 3 ? (int)((0x123233u >> (4 * (b - 4))) & 15u) : (int)((0x122u >> (4 * (b - 3))) & 15u));
+  }
+  static constexpr double TREF = GD == 3 ? 1.0 / 6.0 : 0.5;
+  static constexpr double B = 16.0 / ((GD + 1) * (GD + 2)) * TREF;
+  static constexpr double KVV = (16.0 / ((GD + 1) * (GD + 2)) + 1.0 - 8.0 / (GD + 1)) * TREF;
+  static constexpr double KVE = (16.0 / ((GD + 1) * (GD + 2)) - 4.0 / (GD + 1)) * TREF;
+  static constexpr double KEE = B;
+};
+
+// The NB blocks of one item: row node `aloc` of a cell whose uniform-nu record holds s Ji (rows =
+// s grad lambda_1..d) and sign(mu |J|) in r[GD*GD]; `sl` = accumulator slots of the static columns.
+template <int GD, int NN, int PART>
+__device__ __forceinline__ void bary_blocks(const double* r, int aloc, const int* sl, uint32_t mask, double* acc,
+                                            double rlm, bool negw, int& bad, int maxb) {
+  using Bc = Bary<GD, NN>;
+  constexpr int NV = GD + 1, BS2 = GD * GD;
+  double g[NV][GD];
+#pragma unroll
+  for (int k = 1; k < NV; ++k)
+#pragma unroll
+    for (int d = 0; d < GD; ++d) g[k][d] = r[(k - 1) * GD + d];
+#pragma unroll
+  for (int d = 0; d < GD; ++d) {
+    double t = g[1][d];
+#pragma unroll
+    for (int k = 2; k < NV; ++k) t += g[k][d];
+    g[0][d] = -t;
+  }
+  // row side (dynamic a): its gradient(s), sigma_a and B tau_a(x)
+  const bool av = aloc < NV;
+  int ia = aloc, ja = -1;
+  if constexpr (Bc::P2) {
+    if (!av) { ia = Bc::ep(aloc); ja = Bc::eq(aloc); }
+  }
+  double gi[GD], gj[GD], sig[GD];
+#pragma unroll
+  for (int d = 0; d < GD; ++d) {
+    double vi = g[0][d], vj = g[0][d];
+#pragma unroll
+    for (int k = 1; k < NV; ++k) {
+      vi = ia == k ? g[k][d] : vi;
+      vj = ja == k ? g[k][d] : vj;
+    }
+    gi[d] = vi;
+    gj[d] = av ? 0.0 : vj;
+    sig[d] = gi[d] + gj[d];
+  }
+  const uint32_t rowm = (mask >> (aloc * GD)) & ((1u << GD) - 1);
+#pragma unroll
+  for (int bb = 0; bb < Bc::NB; ++bb) {
+    const int b = Bc::col(PART, bb);
+    const int p = Bc::ep(b), q = Bc::eq(b);
+    const bool bv = b < NV;
+    // G = up gp^T + uq gq^T (P1: up = TREF g_a, uq = 0; P2 vertex column: uq = 0)
+    double up[GD], uq[GD];
+    if constexpr (!Bc::P2) {
+#pragma unroll
+      for (int d = 0; d < GD; ++d) {
+        up[d] = Bc::TREF * gi[d];
+        uq[d] = 0.0;
+      }
+    } else {
+      // u_p = k sigma_a + B tau_a(q), u_q = k sigma_a + B tau_a(p); tau_a(x) = gi if x = ja,
+      // (vertex a: gi, edge a: gj) if x = ia, else 0
+      const double k = bv ? (av ? Bc::KVV : Bc::KVE) : (av ? Bc::KVE : Bc::KEE);
+#pragma unroll
+      for (int d = 0; d < GD; ++d) {
+        const double tq = (q == ia) ? (av ? gi[d] : gj[d]) : (q == ja ? gi[d] : 0.0);
+        up[d] = fma(k, sig[d], Bc::B * tq);
+        const double tp = (p == ia) ? (av ? gi[d] : gj[d]) : (p == ja ? gi[d] : 0.0);
+        uq[d] = bv ? 0.0 : fma(k, sig[d], Bc::B * tp);
+      }
+    }
+    // K = (lam/mu) G + G^T + tr(G) I (mu |J| is in the record's scale s^2), element by element
+    // straight into the accumulator: no G / K arrays live (register pressure)
+    double tr = 0.0;
+#pragma unroll
+    for (int d = 0; d < GD; ++d) tr = fma(up[d], g[p][d], bv ? tr : fma(uq[d], g[q][d], tr));
+    const double sg = negw ? r[BS2] : 1.0;
+    int s = sl[bb];
+    bad |= s < 0;
+    s = s < 0 ? maxb : s;
+    const uint32_t colm = (mask >> (b * GD)) & ((1u << GD) - 1);
+    const bool anybc = __any((rowm | colm) != 0u);
+#pragma unroll
+    for (int i = 0; i < GD; ++i)
+#pragma unroll
+      for (int l = 0; l < GD; ++l) {
+        const double gil = bv ? up[i] * g[p][l] : fma(up[i], g[p][l], uq[i] * g[q][l]);
+        const double gli = bv ? up[l] * g[p][i] : fma(up[l], g[p][i], uq[l] * g[q][i]);
+        double v = i == l ? fma(rlm + 1.0, gil, tr) : fma(rlm, gil, gli);
+        v *= sg;
+        if (anybc && (((rowm >> i) | (colm >> l)) & 1u)) v = 0.0;
+        atomicAdd(&acc[s * BS2 + i * GD + l], v);
+      }
+    __builtin_amdgcn_sched_barrier(0);  // one block at a time: keeps the live set small
+  }
+}
+
 // Items are (adjacency entry, column-node group). NSPLIT groups split the cell's NN column
 // nodes so that a chunk exposes enough independent items to all 256 lanes.
 #ifndef FA_GATHER_WAVES
@@ -1108,6 +1237,19 @@ __device__ __forceinline__ void out_store(const T& v, T* p) {
 #endif
 #ifndef FA_GATHER_SU
 #define FA_GATHER_SU 4  // 16-B values per thread per store batch (LDS reads issued together)
+#endif
+#ifndef FA_GATHER_BARY
+// 1: uniform-nu P1/P2 simplices with a plain slot map use barycentric blocks with static columns
+// (no reference-tensor table; ~30 instead of ~57 FP64 ops per block). Measured slower on config E
+// (57.1 ms at 3 waves/SIMD, 82.5 ms at 4 with spills, vs 49.9 ms for the bank-ordered table path):
+// the items are bound by LDS-atomic bank conflicts, which static columns cannot order away.
+#define FA_GATHER_BARY 0
+#endif
+#ifndef FA_GATHER_FUSEZERO
+#define FA_GATHER_FUSEZERO 0  // 1: each thread zeroes the values it stores (one barrier less; measured 49.8 vs 48.4 ms)
+#endif
+#ifndef FA_GATHER_PRIO
+#define FA_GATHER_PRIO 0  // 1: raise the wave priority while a workgroup streams its chunk out
 #endif
 #ifndef FA_GATHER_APIPE
 #define FA_GATHER_APIPE 0  // measured slower: 5 VGPR spills, config E 50.6 -> 55.2 ms
@@ -1158,8 +1300,11 @@ __device__ __forceinline__ int gather_perm(int jj, int na, int st, float inv) {
   return j < 0 ? j + na : (j >= na ? j - na : j);
 }
 
-template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT>
-__global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
+#ifndef FA_BARY_WAVES
+#define FA_BARY_WAVES FA_GATHER_WAVES
+#endif
+template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT, int VAR = 0>
+__global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES : FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   using R = Rec<GD, NV, NQ, MAT>;
   constexpr int BS2 = GD * GD;
   constexpr int MAXB = kGatherLdsValues / (8 * BS2);
@@ -1176,7 +1321,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   constexpr bool TAB = (MAT != MAT_BLOCKS) && (NEO || !SIMP);  // quadrature tables staged in LDS
   __shared__ double s_w[TAB ? NQ : 1];
   __shared__ double s_dphi[TAB ? NQ * NN * GD : 1];
-  __shared__ double s_ahat[SIMP && !FA_GATHER_AHAT_GLOBAL ? NN * NN * BS2 : 1];
+  __shared__ double s_ahat[SIMP && !FA_GATHER_AHAT_GLOBAL && VAR == 0 ? NN * NN * BS2 : 1];
 
   const int tid = threadIdx.x;
   const int64_t abase = sload(P.A.indptr, P.A.row_begin);  // block index of the window's first value
@@ -1252,7 +1397,7 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   } else if constexpr (NEO) {
     for (int t = tid; t < NQ; t += 256) s_w[t] = P.tab[t];
     for (int t = tid; t < NQ * NN * GD; t += 256) s_dphi[t] = P.tab[NQ + t];
-  } else if constexpr (SIMP && !FA_GATHER_AHAT_GLOBAL) {
+  } else if constexpr (SIMP && !FA_GATHER_AHAT_GLOBAL && VAR == 0) {
     for (int t = tid; t < NN * NN * BS2; t += 256) s_ahat[t] = P.ahat[t];
   } else if constexpr (SIMP) {
   } else {
@@ -1348,6 +1493,13 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   constexpr bool PERM = FA_GATHER_PERMUTE && !NEO;
   // kernels that can run a positional plan (the ordered-slot affine-simplex elasticity path)
   constexpr bool POSM = (MAT == 0 || MAT == MAT_LINU) && SIMP && NN % NSPLIT == 0;
+  // barycentric blocks (bary_blocks): static column parts, one part per half (NSPLIT = 2) of the
+  // workgroup so a wave's items share their code path; needs the plain (unordered) slot map
+  // (a separate instantiation, VAR = 1: sharing one kernel with the table path costs registers)
+  constexpr bool BARY = VAR == 1;
+  static_assert(!BARY || (MAT == MAT_LINU && SIMP && Bary<GD, NN>::NPART == NSPLIT && Bary<GD, NN>::NB == NBG),
+                "barycentric gather: uniform-nu affine P1/P2 simplices");
+  constexpr bool bary_on = BARY;
   auto perm_stride = [&](int na_) { return PERM ? gather_perm_stride(na_) : 1; };
   auto perm = [&](int jj, int na_, int st, float inv) {
     if constexpr (!PERM) return jj;
@@ -1367,7 +1519,13 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   Desc cur = load_desc(idx0);
   fetch(cur);
   stage_meta(cur);
-  zero_acc(cur);
+  if constexpr (FA_GATHER_FUSEZERO) {  // the whole accumulator once; the chunk stores keep it clean
+    double2* acc2 = reinterpret_cast<double2*>(acc);
+    for (int t = tid; t < ((MAXB + 1) * BS2) / 2; t += 256) acc2[t] = make_double2(0.0, 0.0);
+    if ((((MAXB + 1) * BS2) & 1) && tid == 0) acc[(MAXB + 1) * BS2 - 1] = 0.0;
+  } else {
+    zero_acc(cur);
+  }
   int64_t nchunk = idx1;   // chunk k+1 (its descriptor is loaded, its metadata staged next)
   int64_t nnchunk = idx2;  // chunk k+2 (its descriptor is loaded during chunk k)
   Desc nxt = nchunk < P.nchunks ? load_desc(nchunk) : cur;
@@ -1590,6 +1748,17 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
         lds_add_block<GD>(acc, s, K[bb], (mask >> (aloc * GD)) & ((1u << GD) - 1), (mask >> (b * GD)) & ((1u << GD) - 1));
       }
     } else if constexpr (SIMP) {
+      if constexpr (BARY) {
+        {
+          int slb[NBG];
+#pragma unroll
+          for (int bb = 0; bb < NBG; ++bb) slb[bb] = lo + (int)P.slots[(a0 + j) * NN + Bary<GD, NN>::col(part, bb)];
+          const bool negw_b = __any(r[BS2] < 0.0);  // wave-uniform: a cell with mu |J| < 0
+          if (part == 0) bary_blocks<GD, NN, 0>(r, aloc, slb, mask, acc, P.rlm, negw_b, bad, MAXB);
+          else bary_blocks<GD, NN, (Bary<GD, NN>::NPART > 1 ? 1 : 0)>(r, aloc, slb, mask, acc, P.rlm, negw_b, bad, MAXB);
+          return;
+        }
+      }
       // affine simplex: G_ab = |J| Ji^T Ahat_ab Ji  (reference-tensor form)
       constexpr bool LINU = MAT == MAT_LINU;
       // LINU: r = s Ji, r[BS2] = sign; LIN: r = Ji, |J|, lam, mu
@@ -1785,7 +1954,13 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
       it0 += 256;
     }
 #if FA_ABL != 6
-    for (; it0 < nitems; it0 += 256) item(it0, std::false_type{});
+    if constexpr (BARY) {
+      // part = tid / (256 / NSPLIT): whole waves per part; entry jj of the chunk on lane tid % (256 / NSPLIT)
+      constexpr int LPP = 256 / NSPLIT;
+      for (int jj = tid % LPP; jj < na; jj += LPP) item(jj * NSPLIT + tid / LPP, std::false_type{});
+    } else {
+      for (; it0 < nitems; it0 += 256) item(it0, std::false_type{});
+    }
 #endif
   }
 #if FA_ABL == 3
@@ -1863,7 +2038,18 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
     if (acc[tid] == 1.2345e-300) out[tid] = 0.0;  // timing only: no chunk store
     if (false) {
 #endif
-    if (h && tid == 0) out_store(acc[0], out);
+#if FA_GATHER_PRIO
+    __builtin_amdgcn_s_setprio(3);
+#endif
+    // FA_GATHER_FUSEZERO: every accumulator value is read by exactly one thread here, which
+    // writes 0 back after reading it, so the accumulator is clean for the next chunk without a
+    // separate pass and its barrier (values past this chunk were never dirtied: zeroed once at
+    // the start, and items only add inside their chunk)
+    constexpr bool FZ = FA_GATHER_FUSEZERO;
+    if (h && tid == 0) {
+      out_store(acc[0], out);
+      if (FZ) acc[0] = 0.0;
+    }
     const int np = (nv - h) >> 1;
     typedef double dv2 __attribute__((ext_vector_type(2)));
     dv2* out2 = reinterpret_cast<dv2*>(out + h);
@@ -1880,13 +2066,29 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
           else v[u] = reinterpret_cast<const dv2*>(acc)[t];
         }
       }
+      if (FZ) {
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          const int t = t0 + 256 * u;
+          if (t < np) {
+            if (h) { acc[1 + 2 * t] = 0.0; acc[2 + 2 * t] = 0.0; }
+            else reinterpret_cast<dv2*>(acc)[t] = dv2{0.0, 0.0};
+          }
+        }
+      }
 #pragma unroll
       for (int u = 0; u < SU; ++u) {
         const int t = t0 + 256 * u;
         if (t < np) out_store(v[u], out2 + t);
       }
     }
-    if (((nv - h) & 1) && tid == 0) out_store(acc[nv - 1], out + nv - 1);
+    if (((nv - h) & 1) && tid == 0) {
+      out_store(acc[nv - 1], out + nv - 1);
+      if (FZ) acc[nv - 1] = 0.0;
+    }
+#if FA_GATHER_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
 #if FA_ABL == 8
     }
 #endif
@@ -1899,9 +2101,11 @@ __global__ __launch_bounds__(256, FA_GATHER_WAVES) void k_gather(GatherArgs P) {
   gt[6] += 1;
 #endif
   if (nchunk >= P.nchunks) break;
-  __syncthreads();  // the store has read acc
+  if constexpr (!FA_GATHER_FUSEZERO) {
+    __syncthreads();  // the store has read acc
+    zero_acc(nxt);
+  }
   GT_MARK(gt_e);
-  zero_acc(nxt);
   cur = nxt;
   nxt = nn2;
   nchunk = nnchunk;
@@ -2695,6 +2899,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       LAUNCH_CHECK();
       P.ahat = bhat;
       P.trc = 1.0 / (1.0 + rr);
+      P.rlm = rr;
     }
 #if FA_GATHER_TIMING
     {
@@ -2702,7 +2907,16 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_gather_timing), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
     }
 #endif
-    k_gather<GD, NN, NV, NQ, NSPLIT, MAT><<<(unsigned)grid, 256, 0, s>>>(P);
+    bool launched = false;
+    if constexpr (MAT == MAT_LINU && Rec<GD, NV, NQ, MAT>::SIMP && Bary<GD, NN>::NPART == NSPLIT &&
+                  Bary<GD, NN>::NB == (NN + NSPLIT - 1) / NSPLIT && FA_GATHER_BARY && FA_ABL == 0) {
+      if (P.slots && !P.slot_order) {  // barycentric blocks read the plain slot map
+        const int64_t gb = gather_grid(k_gather<GD, NN, NV, NQ, NSPLIT, MAT, 1>, P.nchunks);
+        k_gather<GD, NN, NV, NQ, NSPLIT, MAT, 1><<<(unsigned)gb, 256, 0, s>>>(P);
+        launched = true;
+      }
+    }
+    if (!launched) k_gather<GD, NN, NV, NQ, NSPLIT, MAT><<<(unsigned)grid, 256, 0, s>>>(P);
     LAUNCH_CHECK();
 #if FA_GATHER_TIMING
     {
