@@ -34,6 +34,21 @@ import torch  # noqa: E402
 # 4*nn (dofmap) + 4*nv (geometry dofmap) + 8*gdim*nv (coords) + 8*n_w (E) + 16*ndof^2
 B_E_P2_TET = 4 * 10 + 4 * 4 + 8 * 3 * 4 + 8 * 1 + 16 * 30 * 30  # = 14,560 (bytes_per_cell(CONFIGS["E"]))
 HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, Chip-level parameters)
+FP64_PEAK_TFLOPS = 78.6  # MI355X published FP64 peak (vector = matrix on gfx950; SURVEY.md §8(d) ridge)
+
+
+def flops_per_cell(cfg) -> int:
+    """SURVEY.md §8(d) F_e = n_q (2 ndof^2 n_v + 2 n_v^2 ndof): the B^T D B contraction per cell
+    (n_v = 3 / 6 Voigt components in 2-D / 3-D; 9 for the neo-Hookean F formulation). The AD
+    tangent's own arithmetic (45 second-derivative passes per point) is not counted."""
+    from femasm import fem, mesh
+
+    ct = mesh.CellType[cfg["cell"]]
+    gd = mesh.GDIM[ct]
+    nd = fem.num_nodes_of(ct, cfg["degree"]) * gd
+    nv = 9 if cfg.get("form") == "neo" else (3 if gd == 2 else 6)
+    nq = int(fem.element_info(ct, cfg["degree"], cfg.get("qdeg"))[1])
+    return nq * (2 * nd * nd * nv + 2 * nv * nv * nd)
 
 
 def log(*a):
@@ -285,9 +300,9 @@ def main():
     if world > 1:
         from femasm import parallel
 
-        if args.config != "E":
-            raise SystemExit("N > 1 shards config E's mesh (P2 tets, linear elasticity) only")
-        prob = parallel.SlabProblem(n, rank, world, dev)
+        if args.config not in ("E", "Eneo"):
+            raise SystemExit("N > 1 shards config E's mesh (P2 tets; linear elasticity or neo-Hookean) only")
+        prob = parallel.SlabProblem(n, rank, world, dev, form="neo" if args.config == "Eneo" else "linear")
 
         def step():
             prob.assemble(overlap=not args.no_overlap)
@@ -361,6 +376,10 @@ def main():
     traffic = None if trec is None else round(trec["bytes"] / 1e9, 3)
     traffic_gbps = None if trec is None else trec["bytes"] / (launch_ms * 1e-3) / 1e9
     fracs = {"frac": achieved / HBM_PEAK_GBPS}
+    f_e = flops_per_cell(cfg)
+    tflops = f_e * ncells_local / (launch_ms * 1e-3) / 1e12
+    fracs["flop_frac"] = tflops / FP64_PEAK_TFLOPS
+    compute_bound = cfg.get("form") == "neo"  # AI = F_e / algorithmic bytes is above the FP64 ridge
     if traffic_gbps is not None:
         fracs["traffic_frac"] = traffic_gbps / HBM_PEAK_GBPS
     for k, v in fracs.items():
@@ -388,7 +407,8 @@ def main():
                 cpu_pool.close()
 
     if rank == 0:
-        workload = (f"config {args.config}: {cfg['label']} — linear-elasticity J, {ncells_total} cells, "
+        jform = "neo-Hookean J (device AD tangent)" if cfg.get("form") == "neo" else "linear-elasticity J"
+        workload = (f"config {args.config}: {cfg['label']} — {jform}, {ncells_total} cells, "
                     f"E=E_range[cell%200], nu=0.3, x=0 clamped / x=1 prescribed, BSR(gdim) global matrix")
         if args.config == "E":
             workload = (f"config E mesh, linear elasticity J: unit cube {n}^3 x 6 Kuhn tets, P2 "
@@ -413,13 +433,22 @@ def main():
                       "what": "setup_s = mesh + function space + bcs + sparsity pattern + gather plan, once "
                               "per mesh (the reference's create_matrix is likewise outside its timed region)"},
             "config": {"workload": workload, "method": args.method,
-                       "parallelism": (f"z-slabs x{world}: interface planes first, 2-rank RCCL all-reduce of "
+                       "parallelism": (f"z-slabs x{world}: interface planes first, 2-rank "
+                                       f"{'RCCL' if backend == 'nccl' else backend} all-reduce of "
                                        f"their shared blocks per boundary ({exchange_mb} MB max per rank) "
                                        f"{'after' if args.no_overlap else 'overlapping'} the interior rows")
                        if world > 1 else "single GPU"},
             # per GPU (rank 0 / slowest rank): achieved = algorithmic bytes of the assembly / launch time
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(fracs["frac"], 4), "traffic": traffic,
+            "roofline": {"bound": "mfma" if compute_bound else "hbm",
+                         "achieved": round(tflops, 3) if compute_bound else round(achieved, 1),
+                         "peak": FP64_PEAK_TFLOPS if compute_bound else HBM_PEAK_GBPS,
+                         "unit": "TFLOP/s" if compute_bound else "GB/s",
+                         "frac": round(fracs["flop_frac"] if compute_bound else fracs["frac"], 4), "traffic": traffic,
+                         "hbm": {"achieved_GBps": round(achieved, 1), "frac": round(fracs["frac"], 4)},
+                         "fp64": {"flops_per_cell": f_e, "achieved_TFLOPs": round(tflops, 3),
+                                  "frac": round(fracs["flop_frac"], 4), "peak_TFLOPs": FP64_PEAK_TFLOPS,
+                                  "what": "SURVEY §8(d) F_e (B^T D B contraction; AD passes not counted) "
+                                          "x cells / launch time"},
                          "traffic_GBps": None if traffic_gbps is None else round(traffic_gbps, 1),
                          "traffic_frac": None if traffic_gbps is None else round(fracs["traffic_frac"], 4),
                          "traffic_source": tsrc,

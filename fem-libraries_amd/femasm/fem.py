@@ -49,6 +49,15 @@ def num_nodes_of(ct, p: int) -> int:
             CellType.quadrilateral: (p + 1) ** 2, CellType.hexahedron: (p + 1) ** 3}[ct]
 
 
+def element_info(ct, degree: int, qdeg: int | None = None) -> tuple[int, int]:
+    """(nodes per cell, quadrature points) of the library's element tables (fa_element_info);
+    qdeg None = the degree UFL estimates for the elasticity form."""
+    nn, nq = ctypes.c_int32(0), ctypes.c_int32(0)
+    _lib.check(_lib.load().fa_element_info(int(CellType(ct)), int(degree), -1 if qdeg is None else int(qdeg),
+                                           ctypes.byref(nn), ctypes.byref(nq)), "fa_element_info")
+    return nn.value, nq.value
+
+
 def line_points(p: int) -> np.ndarray:
     """1-D node positions: equispaced (p <= 2) or GLL (p = 3; basix gll_warped)."""
     if p == 3:

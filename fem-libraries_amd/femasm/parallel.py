@@ -26,6 +26,7 @@ CPU, run with nccl = RCCL on MI355X).
 """
 from __future__ import annotations
 
+import copy
 from dataclasses import dataclass
 
 import numpy as np
@@ -182,13 +183,55 @@ def finish_exchange(handle):
         values.view(-1)[fixups] = diagonal
 
 
+def interface_dof_ranges(part: SlabPartition, bs: int) -> dict:
+    """Dof ranges (local numbering) of the lower / upper interface planes: contiguous, since the
+    lattice numbering is plane-major and dofs are blocked (dof = node * bs + comp)."""
+    out = {}
+    for name, rr in (("lower", part.lower), ("upper", part.upper)):
+        if rr is not None:
+            out[name] = (rr[0] * bs, rr[1] * bs)
+    return out
+
+
+def exchange_vector_interfaces(part: SlabPartition, b: torch.Tensor, bs: int, groups, async_op: bool = False):
+    """The ghost update of a slab-assembled vector: VecGhostUpdateBegin/End(ADD_VALUES,
+    SCATTER_REVERSE) of the reference's setF (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:830-831).
+    Each interface plane's dofs are summed over the two ranks sharing it (one 2-rank all-reduce per
+    boundary, the matrix exchange's groups and phase order), after which both copies -- the owner's
+    (lower rank, doc.tex:464) and the neighbour's ghost copy -- hold the complete entries."""
+    import torch.distributed as dist
+
+    steps = []
+    if part.lower is not None:
+        steps.append((part.rank - 1, "lower"))
+    if part.upper is not None:
+        steps.append((part.rank, "upper"))
+    rng = interface_dof_ranges(part, bs)
+    works = []
+    for q, name in sorted(steps, key=lambda s: (s[0] % 2, s[0])):
+        d0, d1 = rng[name]
+        works.append(dist.all_reduce(b[d0:d1], op=dist.ReduceOp.SUM, group=groups[q], async_op=async_op))
+    if async_op:
+        return works
+    return None
+
+
+def slab_state(V, kind: str):
+    """The config-E state: u = 1e-3 (sin pi x, sin pi y, sin pi z) at V's nodes."""
+    if kind != "neo":
+        return None
+    return (1e-3 * torch.sin(torch.pi * V.tabulate_dof_coordinates())).reshape(-1).contiguous()
+
+
 class SlabProblem:
-    """One rank's share of the config-E assembly on its GPU (bench.py at N > 1):
-    3-D P2 linear elasticity on the unit cube, E = E_range[global cell % 200], x = 0 clamped,
-    x = 1 prescribed. ``assemble()`` = local gather assembly + interface exchange."""
+    """One rank's share of the config-E assembly on its GPU (bench.py at N > 1): 3-D P2 on the unit
+    cube, E = E_range[global cell % 200], nu = 0.3, x = 0 clamped, x = 1 prescribed; form
+    "linear" (elasticity, the reference J at d = 0) or "neo" (neo-Hookean, device AD tangent at
+    u = 1e-3 sin(pi x)). ``assemble()`` = local gather assembly + interface exchange;
+    ``assemble_residual()`` = the reference's setF sequence on the slab with the ghost update."""
 
     def __init__(self, n: int, rank: int, world: int, device, degree: int = 2, nu: float = 0.3, groups=None,
-                 cell_type=None, exchange: str = "suffix"):
+                 cell_type=None, exchange: str = "suffix", form: str = "linear", qdeg: int | None = None):
         from . import fem, mesh
         from .la import MatrixCSR
         from .materials import e_range
@@ -214,7 +257,14 @@ class SlabProblem:
         cells_per_layer = n * n * (6 if ct == mesh.CellType.tetrahedron else 1)
         cid = torch.arange(m_asm.num_cells, device=device, dtype=torch.int64) + part.k0 * cells_per_layer
         E = torch.tensor(e_range(), dtype=torch.float64, device=device)[cid % 200]
-        self.a = fem.LinearElasticity(V, E=E, nu=nu)
+        self.form_kind = form
+        self.u = slab_state(V, form)
+        if form == "neo":
+            self.a = fem.NeoHookean(V, E=E, nu=nu, u=self.u, quadrature_degree=2 if qdeg is None else qdeg)
+        elif form == "linear":
+            self.a = fem.LinearElasticity(V, E=E, nu=nu, quadrature_degree=qdeg)
+        else:
+            raise ValueError(f"unknown form {form}")
         left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
         right = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.ones_like(x[0])))
         self.bcs = [fem.dirichletbc(0.0, left, V), fem.dirichletbc([0.01, 0.0, 0.0], right, V)]
@@ -237,7 +287,7 @@ class SlabProblem:
         self.fixups = bc_diagonal_fixups(part, self.A.indptr, self.A.indices, marker, 3)
         self.groups = groups if groups is not None else make_pair_groups(world)
         self.num_cells = m_asm.num_cells
-        self.kernel_name = ("k_cell_records + k_gather<3,10,4,4,2,0> (interface planes, then interior rows) "
+        self.kernel_name = ("k_cell_records + k_gather (interface planes, then interior rows) "
                             "+ 2-rank all_reduce(SUM) per slab boundary overlapping the interior rows")
 
     def assemble(self, overlap: bool = True):
@@ -256,3 +306,24 @@ class SlabProblem:
             sg.rows(self.n_iface)
             exchange_interfaces(self.part, self.A.parts[0][2], self.slices, self.groups, self.fixups,
                                 suffix=self.suffix)
+
+    def assemble_residual(self, f: torch.Tensor | None = None, b: torch.Tensor | None = None) -> torch.Tensor:
+        """The reference's setF on this slab (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:817-845):
+        b = 0; assemble_vector(b, F) over the rank's cells; apply_lifting(b, {J}, {bcs}, {u}, -1);
+        ghost update ADD / REVERSE (exchange_vector_interfaces); set_bc(b, bcs, u, -1). Returns the
+        local dof vector [num_local_nodes * 3]: owned rows complete, interface copies consistent."""
+        from . import fem
+
+        V, a = self.V, self.a
+        if b is None:
+            b = torch.zeros(V.num_dofs, dtype=torch.float64, device=V.mesh.device)
+        else:
+            b.zero_()
+        F = copy.copy(a)  # the residual form: J's coefficients and state, plus the body force f
+        F.f = f
+        fem.assemble_vector(F, b)
+        x0 = None if F.u is None else [F.u]
+        fem.apply_lifting(b, [F], [self.bcs], x0=x0, alpha=-1.0)
+        exchange_vector_interfaces(self.part, b, V.bs, self.groups)
+        fem.set_bc(b, self.bcs, x0=F.u, alpha=-1.0)
+        return b

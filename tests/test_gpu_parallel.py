@@ -24,7 +24,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, n):
+def _worker(rank, world, port, n, kind="linear"):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -35,10 +35,10 @@ def _worker(rank, world, port, n):
     from femasm import fem, parallel
 
     dev = torch.device("cuda", 0)
-    prob = parallel.SlabProblem(n, rank, world, dev)
+    prob = parallel.SlabProblem(n, rank, world, dev, form=kind)
     prob.assemble()
     torch.cuda.synchronize()
-    m, V, a, bcs = bench.build_problem(n, dev)
+    m, V, a, bcs = bench.build_problem(n, dev, cfg=bench.CONFIGS["Eneo" if kind == "neo" else "E"])
     A = fem.assemble_matrix(a, bcs=bcs)
     part = prob.part
     ip_l = prob.A.indptr.cpu().numpy()
@@ -63,8 +63,51 @@ def _worker(rank, world, port, n):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 6), (3, 7)])
-def test_slab_problem_gpu_gloo(world, n):
+@pytest.mark.parametrize("world,n,kind", [(2, 6, "linear"), (3, 7, "linear"), (2, 6, "neo")])
+def test_slab_problem_gpu_gloo(world, n, kind):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    mp.spawn(_worker, args=(world, _port(), n), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _port(), n, kind), nprocs=world, join=True)
+
+
+def _residual_worker(rank, world, port, n, kind):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "fem-libraries_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import copy
+
+    import bench
+    from femasm import fem, parallel
+
+    dev = torch.device("cuda", 0)
+    prob = parallel.SlabProblem(n, rank, world, dev, form=kind)
+    fl = torch.tensor([0.5, -1.0, 2.0], dtype=torch.float64, device=dev).repeat(prob.V.num_nodes)
+    b = prob.assemble_residual(f=fl)
+    torch.cuda.synchronize()
+    # single process, whole mesh: the same setF sequence without a ghost update
+    m, V, a, bcs = bench.build_problem(n, dev, cfg=bench.CONFIGS["Eneo" if kind == "neo" else "E"])
+    F = copy.copy(a)
+    F.f = torch.tensor([0.5, -1.0, 2.0], dtype=torch.float64, device=dev).repeat(V.num_nodes)
+    gb = fem.assemble_vector(F)
+    fem.apply_lifting(gb, [F], [bcs], x0=None if F.u is None else [F.u], alpha=-1.0)
+    fem.set_bc(gb, bcs, x0=F.u, alpha=-1.0)
+    part = prob.part
+    r0, r1 = part.owned_rows
+    off = part.node_offset
+    own, ref = b[r0 * 3:r1 * 3].cpu(), gb[(r0 + off) * 3:(r1 + off) * 3].cpu()
+    scale = float(gb.abs().max())
+    err = float((own - ref).abs().max())
+    assert err <= 1e-12 * scale, f"rank {rank}: residual rel err {err / scale:.2e}"
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,kind", [(2, 6, "linear"), (3, 7, "neo")])
+def test_slab_residual_gpu_gloo(world, n, kind):
+    """Sharded residual (assemble_vector + apply_lifting + ghost update + set_bc) on slabs sharing
+    one GPU equals the single-process residual on every owned dof."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    mp.spawn(_residual_worker, args=(world, _port(), n, kind), nprocs=world, join=True)

@@ -27,7 +27,20 @@ def _bc_marker(xs, bs):
     return on.repeat_interleave(bs).to(torch.int8)
 
 
-def _worker(rank, world, port, n, async_op=False, mode="rows"):
+def _state(xs, kind):
+    """The config-E neo-Hookean state u = 1e-3 sin(pi x) per dof (None for the linear form)."""
+    if kind != "neo":
+        return None
+    return (1e-3 * torch.sin(torch.pi * xs)).reshape(-1).numpy()
+
+
+def _assemble(O, kind, p, cells, geom, x, lam, mu, u, ip, ix, bc):
+    if kind == "neo":
+        return O.assemble_neohookean(-4, p, cells, geom, x, lam, mu, u, ip, ix, bc=bc, diag=1.0, qdeg=2)
+    return O.assemble_elasticity(-4, p, cells, geom, x, lam, mu, ip, ix, bc=bc, diag=1.0)
+
+
+def _worker(rank, world, port, n, async_op=False, mode="rows", kind="linear"):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -52,8 +65,8 @@ def _worker(rank, world, port, n, async_op=False, mode="rows"):
     marker = _bc_marker(xl, bs)
     cid = np.arange(m_asm.num_cells) + part.k0 * n * n * 6
     lam, mu = O.lame(e_range()[cid % 200], 0.3)
-    vals = O.assemble_elasticity(-4, p, dof_asm, m_asm.cells.numpy(), m_asm.x.numpy(), lam, mu, indptr, indices,
-                                 bc=marker.numpy(), diag=1.0)
+    vals = _assemble(O, kind, p, dof_asm, m_asm.cells.numpy(), m_asm.x.numpy(), lam, mu, _state(xl, kind), indptr,
+                     indices, marker.numpy())
     ip_t, ix_t = torch.from_numpy(indptr), torch.from_numpy(indices)
     w0, w1 = int(indptr[part.row_begin]), int(indptr[part.row_end])
     window = torch.from_numpy(vals[w0:w1].copy())
@@ -72,9 +85,10 @@ def _worker(rank, world, port, n, async_op=False, mode="rows"):
     dof = fem._structured_dofmap(m, p)[0].numpy()
     nglob = (p * n + 1) ** 3
     gip, gix = O.sparsity(dof, nglob)
-    gmarker = _bc_marker(fem._structured_node_coordinates(m, p), bs).numpy()
+    gx = fem._structured_node_coordinates(m, p)
+    gmarker = _bc_marker(gx, bs).numpy()
     glam, gmu = O.lame(e_range()[np.arange(m.num_cells) % 200], 0.3)
-    gvals = O.assemble_elasticity(-4, p, dof, m.cells.numpy(), m.x.numpy(), glam, gmu, gip, gix, bc=gmarker, diag=1.0)
+    gvals = _assemble(O, kind, p, dof, m.cells.numpy(), m.x.numpy(), glam, gmu, _state(gx, kind), gip, gix, gmarker)
     scale = np.abs(gvals).max()
     err = 0.0
     for r in range(part.row_begin, part.row_end):  # owned rows and the ghost copy of the lower interface
@@ -97,6 +111,87 @@ def _worker(rank, world, port, n, async_op=False, mode="rows"):
                                                    (4, 4, True, "suffix"), (3, 5, True, "suffix")])
 def test_slab_exchange_gloo(world, n, async_op, mode):
     mp.spawn(_worker, args=(world, _free_port(), n, async_op, mode), nprocs=world, join=True)
+
+
+@pytest.mark.parametrize("world,n", [(2, 4), (3, 5)])
+def test_slab_exchange_neohookean_gloo(world, n):
+    """Config E's physics on slabs: the neo-Hookean tangent at u = 1e-3 sin(pi x) (oracle closed form
+    per rank), suffix exchange overlapped: owned rows equal the global assembly."""
+    mp.spawn(_worker, args=(world, _free_port(), n, True, "suffix", "neo"), nprocs=world, join=True)
+
+
+def _residual_worker(rank, world, port, n, kind):
+    """setF on slabs (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:817-845): each rank assembles
+    the residual and the lifting of its own cells (oracle), the interface planes are summed with the
+    slab neighbour (parallel.exchange_vector_interfaces = VecGhostUpdate ADD/REVERSE, :830-831),
+    then set_bc. Owned entries must equal the global residual."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "fem-libraries_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from femasm import fem, mesh, parallel
+    from femasm.materials import e_range
+    from oracle import oracle as O
+
+    p, bs, L, ct = 2, 3, (1.0, 1.0, 1.0), mesh.CellType.tetrahedron
+    okind = 2 if kind == "neo" else 0
+    qdeg = 2 if kind == "neo" else -1
+
+    def setf(cells, geom, x, lam, mu, xs, nnodes):
+        marker = _bc_marker(xs, bs).numpy()
+        g = np.zeros(nnodes * bs)
+        right = torch.isclose(xs[:, 0], torch.ones_like(xs[:, 0])).numpy()
+        g[np.flatnonzero(right) * bs] = 0.01
+        u = _state(xs, kind)
+        if u is None:
+            u = 0.002 * np.cos(3.0 * xs.numpy()).reshape(-1)  # a nonzero state for the linear residual
+        f = np.tile([0.5, -1.0, 2.0], nnodes)
+        b = np.zeros(nnodes * bs)
+        r = O.assemble_residual(-4, p, cells, geom, x, lam, mu, u=u, f=f, kind=okind, qdeg=qdeg)
+        b[:r.size] = r
+        b = O.apply_lifting(-4, p, cells, geom, x, lam, mu, b, marker, g, x0=u, alpha=-1.0, u=u, kind=okind,
+                            qdeg=qdeg)
+        return b, marker, g, u
+
+    part = parallel.SlabPartition((n, n, n), p, rank, world)
+    m_asm = mesh.create_box(L, (n, n, n), ct, z_range=(part.k0, part.k1))
+    nloc = part.num_local_nodes
+    dof_asm = part.to_local(fem._structured_dofmap(m_asm, p)[0]).numpy()
+    xs = fem._structured_node_coordinates(m_asm, p)
+    xl = xs[part.node_offset:part.node_offset + nloc]
+    cid = np.arange(m_asm.num_cells) + part.k0 * n * n * 6
+    lam, mu = O.lame(e_range()[cid % 200], 0.3)
+    b, marker, g, u = setf(dof_asm, m_asm.cells.numpy(), m_asm.x.numpy(), lam, mu, xl, nloc)
+    bt = torch.from_numpy(b)
+    parallel.exchange_vector_interfaces(part, bt, bs, parallel.make_pair_groups(world))
+    b = bt.numpy()
+    b[marker != 0] = -1.0 * (g - u)[marker != 0]  # set_bc(b, bcs, u, -1)
+
+    m = mesh.create_unit_cube(n, n, n, ct)
+    dof = fem._structured_dofmap(m, p)[0].numpy()
+    gx = fem._structured_node_coordinates(m, p)
+    glam, gmu = O.lame(e_range()[np.arange(m.num_cells) % 200], 0.3)
+    gb, gmarker, gg, gu = setf(dof, m.cells.numpy(), m.x.numpy(), glam, gmu, gx, (p * n + 1) ** 3)
+    gb[gmarker != 0] = -1.0 * (gg - gu)[gmarker != 0]
+    r0, r1 = part.owned_rows
+    own = b[r0 * bs:r1 * bs]
+    ref = gb[(r0 + part.node_offset) * bs:(r1 + part.node_offset) * bs]
+    scale = np.abs(gb).max()
+    assert np.abs(own - ref).max() <= 1e-12 * scale, f"rank {rank}: {np.abs(own - ref).max() / scale:.2e}"
+    # the ghost copy of the lower interface plane is consistent too
+    if part.lower is not None:
+        l0, l1 = part.lower
+        np.testing.assert_allclose(b[l0 * bs:l1 * bs], gb[(l0 + part.node_offset) * bs:(l1 + part.node_offset) * bs],
+                                   rtol=0, atol=1e-12 * scale)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,kind", [(2, 4, "linear"), (3, 5, "linear"), (2, 4, "neo")])
+def test_slab_residual_ghost_update_gloo(world, n, kind):
+    mp.spawn(_residual_worker, args=(world, _free_port(), n, kind), nprocs=world, join=True)
 
 
 def test_slab_partition_covers_all_layers():
