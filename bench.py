@@ -382,8 +382,11 @@ def main():
     compute_bound = cfg.get("form") == "neo"  # AI = F_e / algorithmic bytes is above the FP64 ridge
     if traffic_gbps is not None:
         fracs["traffic_frac"] = traffic_gbps / HBM_PEAK_GBPS
+    # the fractions reported as measured must be physical; F_e is the quadrature contraction's
+    # flop count, a model for kernels that do not run it (the affine reference-tensor gathers)
     for k, v in fracs.items():
-        assert v <= 1.0, f"roofline {k} = {v:.3f} > 1: a byte count or a time is wrong"
+        if k != "flop_frac" or compute_bound:
+            assert v <= 1.0, f"roofline {k} = {v:.3f} > 1: a byte count or a time is wrong"
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -447,8 +450,10 @@ def main():
                          "hbm": {"achieved_GBps": round(achieved, 1), "frac": round(fracs["frac"], 4)},
                          "fp64": {"flops_per_cell": f_e, "achieved_TFLOPs": round(tflops, 3),
                                   "frac": round(fracs["flop_frac"], 4), "peak_TFLOPs": FP64_PEAK_TFLOPS,
-                                  "what": "SURVEY §8(d) F_e (B^T D B contraction; AD passes not counted) "
-                                          "x cells / launch time"},
+                                  "what": ("SURVEY §8(d) F_e (B^T D B contraction; AD passes not counted) "
+                                           "x cells / launch time") + ("" if compute_bound else
+                                          ": a model here -- the affine gathers form blocks from "
+                                          "reference tensors, not from the quadrature contraction")},
                          "traffic_GBps": None if traffic_gbps is None else round(traffic_gbps, 1),
                          "traffic_frac": None if traffic_gbps is None else round(fracs["traffic_frac"], 4),
                          "traffic_source": tsrc,

@@ -288,6 +288,30 @@ inline bool tabulate(int ct, int p, const Quadrature& Q, std::vector<double>& va
   return true;
 }
 
+// 1-D matrices of a tensor element on [0, 1] with the n-point Gauss rule of make_quadrature(ct, qdeg)
+// (n = (qdeg + 2) / 2 per direction), [3][p+1][p+1]: S_ij = int l_i' l_j', M_ij = int l_i l_j,
+// C_ij = int l_i' l_j. On an affine (parallelepiped) cell the reference grad-grad tensor of
+// nodes a = (a0, a1, a2), b factorises: Ahat_ab[j][l] = prod_d F_d with F_d = S (d = j = l),
+// C[a_d][b_d] (d = j != l), C[b_d][a_d] (d = l != j), M (otherwise) -- equal to the tensor rule's
+// sum (which is exact for these degrees) up to rounding.
+inline void tensor_1d_mats(int p, int qdeg, std::vector<double>& out) {
+  std::vector<double> x, w;
+  gauss_legendre_01((qdeg + 2) / 2, x, w);
+  std::vector<double> r = line_points(p);
+  const int n1 = p + 1;
+  out.assign(3 * n1 * n1, 0.0);
+  for (size_t q = 0; q < x.size(); ++q) {
+    double v[4], dv[4];
+    for (int i = 0; i < n1; ++i) lagrange_1d(r, i, x[q], v[i], dv[i]);
+    for (int i = 0; i < n1; ++i)
+      for (int j = 0; j < n1; ++j) {
+        out[0 * n1 * n1 + i * n1 + j] += w[q] * dv[i] * dv[j];
+        out[1 * n1 * n1 + i * n1 + j] += w[q] * v[i] * v[j];
+        out[2 * n1 * n1 + i * n1 + j] += w[q] * dv[i] * v[j];
+      }
+  }
+}
+
 // Everything a kernel needs about one (cell, degree, quadrature degree) combination.
 struct ElementTables {
   int ct = 0, p = 0, td = 0, nn = 0, nv = 0, nq = 0, qdeg = 0;

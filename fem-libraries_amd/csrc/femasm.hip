@@ -76,6 +76,8 @@ struct DevTables {
   const double* phi;
   const double* gphi;
   const double* ahat;  // simplex only: [nn][nn][td][td] = sum_q w_q dphi_a(q) dphi_b(q)^T
+  const double* t1d;   // tensor cells: 1-D matrices S, M, C [3][p+1][p+1] (tensor_1d_mats)
+  const double* lat;   // tensor cells: node lattice code a0 + 8 a1 + 64 a2 per node (as doubles)
   int ndoubles;
 };
 
@@ -116,6 +118,17 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
             h.push_back(v);
           }
   }
+  // tensor cells: 1-D matrices of the affine fast path and the node lattice codes
+  size_t off_t1d = 0, off_lat = 0;
+  if (!is_simplex(ct)) {
+    std::vector<double> t1;
+    tensor_1d_mats(p, qd, t1);
+    off_t1d = h.size();
+    h.insert(h.end(), t1.begin(), t1.end());
+    off_lat = h.size();
+    std::vector<int> L = tensor_node_lattice(ct, p);
+    for (int a = 0; a < T.nn; ++a) h.push_back((double)(L[3 * a] + 8 * L[3 * a + 1] + 64 * L[3 * a + 2]));
+  }
   double* d = nullptr;
   HIP_TRY(hipMalloc(&d, h.size() * sizeof(double)));
   HIP_TRY(hipMemcpy(d, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -127,6 +140,8 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
   D.phi = D.gdphi + (size_t)T.nq * T.nv * T.td;
   D.gphi = D.phi + (size_t)T.nq * T.nn;
   D.ahat = is_simplex(ct) ? d + off_ahat : nullptr;
+  D.t1d = is_simplex(ct) ? nullptr : d + off_t1d;
+  D.lat = is_simplex(ct) ? nullptr : d + off_lat;
   D.ndoubles = (int)h.size();
   g_tabs[key] = D;
   *out = D;
@@ -227,6 +242,25 @@ __device__ __forceinline__ double simplex_geometry(const MeshView& M, int64_t c,
 #pragma unroll
   for (int k = 0; k < GD; ++k) {
     int vk = g[k + 1];
+#pragma unroll
+    for (int i = 0; i < GD; ++i) J[i][k] = M.x[(int64_t)vk * GD + i] - x0[i];
+  }
+  return jac_inv<GD>(J, Ji);
+}
+
+// Affine tensor cell (parallelogram / parallelepiped): J columns are the edges from vertex 0 to the
+// vertices at xi = e_k (basix order: vertices 1, 2 and, in 3-D, 4). Only valid where the cell is
+// affine (fa_plan_gather checks every cell and sets FA_PLAN_AFFINE).
+template <int GD, int NV>
+__device__ __forceinline__ double affine_tensor_geometry(const MeshView& M, int64_t c, double (&Ji)[GD][GD]) {
+  const int32_t* g = M.geom + c * NV;
+  double x0[GD], J[GD][GD];
+  const int v0 = g[0];
+#pragma unroll
+  for (int i = 0; i < GD; ++i) x0[i] = M.x[(int64_t)v0 * GD + i];
+#pragma unroll
+  for (int k = 0; k < GD; ++k) {
+    const int vk = g[1 << k];
 #pragma unroll
     for (int i = 0; i < GD; ++i) J[i][k] = M.x[(int64_t)vk * GD + i] - x0[i];
   }
@@ -835,16 +869,21 @@ constexpr int MAT_BLOCKS = 9;
 // (and the sign of mu |J|), the table B_ab = r Ahat_ab + Ahat_ab^T, and
 // K = H + tr(H) / (1 + r) I with H = (s Ji)^T B (s Ji): 19 fewer FP64 ops per block
 constexpr int MAT_LINU = 10;
+// linear elasticity, uniform nu, on affine tensor cells (parallelograms / parallelepipeds): the
+// uniform-nu record of an affine simplex (s Ji, sign) and a reference tensor that factorises into
+// 1-D matrices (tensor_1d_mats), computed per block instead of read from a table -- the simplex
+// gather for Q1-Q3 hexahedra of a structured mesh, with no element-matrix store
+constexpr int MAT_AFFT = 11;
 
 template <int GD, int NV, int NQ, int MAT>
 struct Rec {
-  static constexpr bool SIMP = (NV == GD + 1);
+  static constexpr bool SIMP = (NV == GD + 1) || MAT == MAT_AFFT;  // affine: one Jacobian per cell
   static constexpr int N = GD * GD;
   static constexpr int NTRI = N * (N + 1) / 2;  // stored upper triangle of the tangent
   // LIN simplex: Ji[GD*GD], wdet, lam, mu | LINU (simplex): s Ji[GD*GD], sign(mu wdet) | LIN tensor: NQ x (Ji[GD*GD], wdet), lam, mu |
   // DAMAGE (P1 tri): g[3][2], w, H[3][3] | NEO (simplex): Ji[GD*GD], wdet, NQ x A_q upper triangle
   static constexpr int RAW = MAT == MAT_BLOCKS ? 2
-                             : MAT == MAT_LINU ? GD * GD + 1
+                             : (MAT == MAT_LINU || MAT == MAT_AFFT) ? GD * GD + 1
                              : MAT == FA_ASYM_DAMAGE ? 16
                              : MAT == FA_NEO_HOOKEAN ? N + 1 + NQ * NTRI
                                                      : (SIMP ? GD * GD + 3 : NQ * (GD * GD + 1) + 2);
@@ -878,6 +917,9 @@ struct GatherArgs {
   const double* ahat; // simplex reference tensor [nn][nn][GD][GD] (MAT_LINU: the table B)
   double trc;         // MAT_LINU: 1 / (1 + lam / mu)
   double rlm;         // MAT_LINU: lam / mu
+  int affine;         // every cell affine (plan cell_flags & FA_PLAN_AFFINE): tensor cells may use MAT_AFFT
+  const double* t1d;  // MAT_AFFT: 1-D matrices S, M, C [3][p+1][p+1]
+  const double* lat;  // MAT_AFFT: node lattice codes a0 + 8 a1 + 64 a2
   const double* rec;  // [ncells][Rec::SIZE]
   const uint32_t* bcmask;  // [ncells] or NULL
   int* err;
@@ -929,12 +971,12 @@ __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, co
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) r[7 + 3 * i + j] = H[i][j];
-  } else if constexpr (MAT == MAT_LINU) {
-    static_assert(R::SIMP, "uniform-nu records: affine simplices");
+  } else if constexpr (MAT == MAT_LINU || MAT == MAT_AFFT) {
+    static_assert(R::SIMP, "uniform-nu records: affine cells");
     double lam, mu;
     cell_lame(F, c, lam, mu);
     double Ji[GD][GD];
-    const double s2 = mu * fabs(simplex_geometry<GD>(M, c, Ji));
+    const double s2 = mu * fabs(MAT == MAT_AFFT ? affine_tensor_geometry<GD, NV>(M, c, Ji) : simplex_geometry<GD>(M, c, Ji));
     const double sc = sqrt(fabs(s2));
 #pragma unroll
     for (int i = 0; i < GD; ++i)
@@ -983,11 +1025,19 @@ __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, co
   if (bcmask) {
     uint32_t m = 0;
     const int32_t* cn = M.cells + c * NN;
+    if constexpr (NN * GD <= 32) {
 #pragma unroll
-    for (int b = 0; b < NN; ++b) {
-      int64_t n = cn[b];
+      for (int b = 0; b < NN; ++b) {
+        int64_t n = cn[b];
 #pragma unroll
-      for (int j = 0; j < GD; ++j) m |= (bc[n * GD + j] ? 1u : 0u) << (b * GD + j);
+        for (int j = 0; j < GD; ++j) m |= (bc[n * GD + j] ? 1u : 0u) << (b * GD + j);
+      }
+    } else {  // too many dofs for a bit mask: "the cell touches a constrained dof" (the gather looks them up)
+      for (int b = 0; b < NN; ++b) {
+        int64_t n = cn[b];
+#pragma unroll
+        for (int j = 0; j < GD; ++j) m |= bc[n * GD + j] ? 1u : 0u;
+      }
     }
     bcmask[c] = m;
   }
@@ -1321,7 +1371,11 @@ __global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES : FA_GATHER_WAVES) vo
   constexpr bool TAB = (MAT != MAT_BLOCKS) && (NEO || !SIMP);  // quadrature tables staged in LDS
   __shared__ double s_w[TAB ? NQ : 1];
   __shared__ double s_dphi[TAB ? NQ * NN * GD : 1];
-  __shared__ double s_ahat[SIMP && !FA_GATHER_AHAT_GLOBAL && VAR == 0 ? NN * NN * BS2 : 1];
+  constexpr bool AFFT = MAT == MAT_AFFT;
+  __shared__ double s_ahat[SIMP && !AFFT && !FA_GATHER_AHAT_GLOBAL && VAR == 0 ? NN * NN * BS2 : 1];
+  constexpr int P1D = AFFT ? (NN == 8 || NN == 4 ? 2 : (NN == 27 || NN == 9 ? 3 : 4)) : 1;  // 1-D nodes
+  __shared__ double s_t1d[AFFT ? 3 * P1D * P1D : 1];
+  __shared__ int s_lat[AFFT ? NN : 1];
 
   const int tid = threadIdx.x;
   const int64_t abase = sload(P.A.indptr, P.A.row_begin);  // block index of the window's first value
@@ -1397,6 +1451,9 @@ __global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES : FA_GATHER_WAVES) vo
   } else if constexpr (NEO) {
     for (int t = tid; t < NQ; t += 256) s_w[t] = P.tab[t];
     for (int t = tid; t < NQ * NN * GD; t += 256) s_dphi[t] = P.tab[NQ + t];
+  } else if constexpr (AFFT) {
+    for (int t = tid; t < 3 * P1D * P1D; t += 256) s_t1d[t] = P.t1d[t];
+    for (int t = tid; t < NN; t += 256) s_lat[t] = (int)P.lat[t];
   } else if constexpr (SIMP && !FA_GATHER_AHAT_GLOBAL && VAR == 0) {
     for (int t = tid; t < NN * NN * BS2; t += 256) s_ahat[t] = P.ahat[t];
   } else if constexpr (SIMP) {
@@ -1492,14 +1549,14 @@ __global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES : FA_GATHER_WAVES) vo
   // (neo-Hookean: measured 3 % faster without the permutation, n = 120)
   constexpr bool PERM = FA_GATHER_PERMUTE && !NEO;
   // kernels that can run a positional plan (the ordered-slot affine-simplex elasticity path)
-  constexpr bool POSM = (MAT == 0 || MAT == MAT_LINU) && SIMP && NN % NSPLIT == 0;
+  constexpr bool POSM = (MAT == 0 || MAT == MAT_LINU || (MAT == MAT_AFFT && NN * GD <= 32)) && SIMP &&
+                        NN % NSPLIT == 0;
   // barycentric blocks (bary_blocks): static column parts, one part per half (NSPLIT = 2) of the
   // workgroup so a wave's items share their code path; needs the plain (unordered) slot map
   // (a separate instantiation, VAR = 1: sharing one kernel with the table path costs registers)
   constexpr bool BARY = VAR == 1;
   static_assert(!BARY || (MAT == MAT_LINU && SIMP && Bary<GD, NN>::NPART == NSPLIT && Bary<GD, NN>::NB == NBG),
                 "barycentric gather: uniform-nu affine P1/P2 simplices");
-  constexpr bool bary_on = BARY;
   auto perm_stride = [&](int na_) { return PERM ? gather_perm_stride(na_) : 1; };
   auto perm = [&](int jj, int na_, int st, float inv) {
     if constexpr (!PERM) return jj;
@@ -1760,7 +1817,7 @@ __global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES : FA_GATHER_WAVES) vo
         }
       }
       // affine simplex: G_ab = |J| Ji^T Ahat_ab Ji  (reference-tensor form)
-      constexpr bool LINU = MAT == MAT_LINU;
+      constexpr bool LINU = MAT == MAT_LINU || MAT == MAT_AFFT;
       // LINU: r = s Ji, r[BS2] = sign; LIN: r = Ji, |J|, lam, mu
       const double wdet = LINU ? 1.0 : r[BS2], lam = LINU ? 0.0 : r[LINU ? 0 : BS2 + 1] * wdet,
                    mu = LINU ? 0.0 : r[LINU ? 0 : BS2 + 2] * wdet;
@@ -1793,8 +1850,12 @@ __global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES : FA_GATHER_WAVES) vo
       const unsigned long long gt_i1 = __builtin_amdgcn_s_memtime();
       gt[7] += gt_i1 - gt_i0;
 #endif
-      const uint32_t rowm = (mask >> (aloc * GD)) & ((1u << GD) - 1);
+      // constrained-dof bits: from the cell's mask, or -- cells with more dofs than mask bits -- from
+      // the chunk row's bits and the column node's markers (only in waves holding such a cell)
+      constexpr bool BIGM = NN * GD > 32;
+      const uint32_t rowm = BIGM ? (mask ? (uint32_t)s_rowbc[lr] : 0u) : (mask >> (aloc * GD)) & ((1u << GD) - 1);
       const double* Ah0 = (FA_GATHER_AHAT_GLOBAL ? P.ahat : s_ahat) + aloc * NN * BS2;
+      const int alat = AFFT ? s_lat[aloc] : 0;
       // Reference-tensor reads one block ahead: block bb+1's table entry is read before block
       // bb's adds are issued, so the wait for it (an in-order lgkmcnt) does not also wait for
       // those nine LDS atomics to complete (FA_GATHER_APIPE=0: read at the top of each block)
@@ -1820,8 +1881,38 @@ __global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES : FA_GATHER_WAVES) vo
         const double* Ahp = Ahr;
 #else
         double Ahc[BS2];
+        if constexpr (AFFT) {
+          // reference tensor of an affine tensor cell from the 1-D matrices, then the uniform-nu
+          // table entry B = (lam/mu) Ahat + Ahat^T
+          const int blat = s_lat[b];
+          double Sd[GD], Md[GD], Cd[GD], Ctd[GD];
 #pragma unroll
-        for (int e = 0; e < BS2; ++e) Ahc[e] = APIPE ? Ahn[e] : Ah0[b * BS2 + e];
+          for (int d = 0; d < GD; ++d) {
+            const int ad = (alat >> (3 * d)) & 7, bd = (blat >> (3 * d)) & 7;
+            Sd[d] = s_t1d[ad * P1D + bd];
+            Md[d] = s_t1d[P1D * P1D + ad * P1D + bd];
+            Cd[d] = s_t1d[2 * P1D * P1D + ad * P1D + bd];
+            Ctd[d] = s_t1d[2 * P1D * P1D + bd * P1D + ad];
+          }
+          double A[GD][GD];
+#pragma unroll
+          for (int jd = 0; jd < GD; ++jd)
+#pragma unroll
+            for (int ld = 0; ld < GD; ++ld) {
+              double v = 1.0;
+#pragma unroll
+              for (int d = 0; d < GD; ++d)
+                v *= (d == jd && d == ld) ? Sd[d] : (d == jd ? Cd[d] : (d == ld ? Ctd[d] : Md[d]));
+              A[jd][ld] = v;
+            }
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int k = 0; k < GD; ++k) Ahc[i * GD + k] = fma(P.rlm, A[i][k], A[k][i]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < BS2; ++e) Ahc[e] = APIPE ? Ahn[e] : Ah0[b * BS2 + e];
+        }
         const double* Ahp = Ahc;
 #endif
         double T[GD][GD];  // T = Ahat Ji
@@ -1882,7 +1973,18 @@ __global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES : FA_GATHER_WAVES) vo
 #pragma unroll
           for (int jj = 0; jj < GD; ++jj) abl_sink += K[i][jj] * (double)s;
 #else
-        lds_add_block<GD>(acc, s, K, rowm, (mask >> (b * GD)) & ((1u << GD) - 1));
+        uint32_t colm;
+        if constexpr (BIGM) {
+          colm = 0u;
+          if (mask && s < MAXB) {
+            const int64_t nb_ = cols[s];
+#pragma unroll
+            for (int jd = 0; jd < GD; ++jd) colm |= (P.bc[nb_ * GD + jd] ? 1u : 0u) << jd;
+          }
+        } else {
+          colm = (mask >> (b * GD)) & ((1u << GD) - 1);
+        }
+        lds_add_block<GD>(acc, s, K, rowm, colm);
 #endif
       }
 #if FA_GATHER_TIMING
@@ -2555,7 +2657,7 @@ __global__ void k_plan_perm(const int64_t* __restrict__ row_start, const int64_t
                             const int64_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj_idx,
                             int64_t nchunks, const uint16_t* __restrict__ src, uint16_t* __restrict__ eperm,
                             int32_t* __restrict__ eadj) {
-  constexpr int EQ = 16 / NSPLIT;              // entries per quarter (host: only for 16 % NSPLIT == 0)
+  constexpr int EQ = NSPLIT <= 16 ? 16 / NSPLIT : 1;  // entries per quarter (host: only for 16 % NSPLIT == 0)
   constexpr int MQ = kGatherMaxAdj / EQ;       // quarters per chunk, at most
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nchunks;
        c += (int64_t)gridDim.x * blockDim.x) {
@@ -2605,7 +2707,14 @@ __global__ void k_plan_perm(const int64_t* __restrict__ row_start, const int64_t
 #ifndef FA_P2TET_NSPLIT
 #define FA_P2TET_NSPLIT 2  // measured best with the reference-tensor blocks (n=120 sweep)
 #endif
-static int lin_simplex_nsplit(int ct, int p, int nq) {
+static int lin_simplex_nsplit(int ct, int p, int nq, bool affine = false) {
+  // affine hexahedra (MAT_AFFT): Q1 / Q2 / Q3 with their default rules
+  if (affine && ct == FA_HEXAHEDRON && p == 1 && nq == 8) return 2;
+  if (affine && ct == FA_HEXAHEDRON && p == 2 && nq == 27) return 9;
+  if (affine && ct == FA_HEXAHEDRON && p == 3 && nq == 64) return 32;
+  if (affine && ct == FA_QUADRILATERAL && p == 1 && nq == 4) return 1;
+  if (affine && ct == FA_QUADRILATERAL && p == 2 && nq == 9) return 3;
+  if (affine && ct == FA_QUADRILATERAL && p == 3 && nq == 16) return 4;
   if (ct == FA_TRIANGLE && p == 1 && nq == 1) return 1;
   if (ct == FA_TRIANGLE && p == 2 && nq == 3) return 2;
   if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return 2;
@@ -2623,7 +2732,7 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   plan->eadj = nullptr;
   DevTables T;
   if ((rc = get_tables(mesh->cell_type, mesh->degree, -1, &T))) return rc;
-  const int ns = lin_simplex_nsplit(mesh->cell_type, mesh->degree, T.nq);
+  const int ns = lin_simplex_nsplit(mesh->cell_type, mesh->degree, T.nq, (plan->cell_flags & FA_PLAN_AFFINE) != 0);
   if (ns == 0 || plan->nchunks <= 0) return FA_OK;  // no kernel reads an ordered map: keep plain slots
   // ordered entries pack (b << 10) | chunk-relative position (k_order_slots): keep the plain map
   // for a plan whose chunks could hold 1024 blocks or more
@@ -2665,6 +2774,12 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   else if (mesh->nn == 10 && ns == 2) ORD(10, 2);
   else if (mesh->nn == 10 && ns == 5) ORD(10, 5);
   else if (mesh->nn == 10 && ns == 1) ORD(10, 1);
+  else if (mesh->nn == 8 && ns == 2) ORD(8, 2);
+  else if (mesh->nn == 27 && ns == 9) ORD(27, 9);
+  else if (mesh->nn == 64 && ns == 32) ORD(64, 32);
+  else if (mesh->nn == 4 && ns == 1) ORD(4, 1);
+  else if (mesh->nn == 9 && ns == 3) ORD(9, 3);
+  else if (mesh->nn == 16 && ns == 4) ORD(16, 4);
   else ok = false;
 #undef ORD
   if (src) HIP_TRY(hipFreeAsync(src, s));
@@ -2686,6 +2801,34 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   plan->slot_order = ns;
   plan->eadj = posn ? eadj : nullptr;
   return FA_OK;
+}
+
+// Tensor cells: is every cell affine (x_v = x_0 + J xi_v at all vertices, J from vertices 1, 2, 4)?
+// Sets *nonaffine when one is not (tolerance: 1e-12 of the cell's size).
+template <int GD>
+__global__ void k_check_affine(MeshView M, int* nonaffine) {
+  constexpr int NV = 1 << GD;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < M.ncells; c += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t* g = M.geom + c * NV;
+    double x[NV][GD];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int i = 0; i < GD; ++i) x[v][i] = M.x[(int64_t)g[v] * GD + i];
+    double h = 0.0, dev = 0.0;
+#pragma unroll
+    for (int v = 1; v < NV; ++v)
+#pragma unroll
+      for (int i = 0; i < GD; ++i) {
+        double pred = x[0][i];
+#pragma unroll
+        for (int k = 0; k < GD; ++k)
+          if ((v >> k) & 1) pred += x[1 << k][i] - x[0][i];
+        dev = fmax(dev, fabs(x[v][i] - pred));
+        h = fmax(h, fabs(x[v][i] - x[0][i]));
+      }
+    if (dev > 1e-12 * h) atomicOr(nonaffine, 1);
+  }
 }
 
 extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int64_t* row_start,
@@ -2731,6 +2874,21 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
   HIP_TRY(hipStreamSynchronize(s));
   plan->nchunks = (int64_t)rs.size() - 1;
   plan->row_start = row_start;
+  plan->cell_flags = 0;
+  if ((mesh->cell_type == FA_HEXAHEDRON || mesh->cell_type == FA_QUADRILATERAL) && mesh->ncells > 0) {
+    MeshView M{mesh->cells, mesh->geom, mesh->x, mesh->ncells, mesh->nnodes, mesh->nn, mesh->nv, mesh->gdim};
+    int* dna = nullptr;
+    int na_h = 1;
+    HIP_TRY(hipMallocAsync((void**)&dna, sizeof(int), s));
+    HIP_TRY(hipMemsetAsync(dna, 0, sizeof(int), s));
+    if (mesh->gdim == 3) k_check_affine<3><<<grid_for(mesh->ncells), 256, 0, s>>>(M, dna);
+    else k_check_affine<2><<<grid_for(mesh->ncells), 256, 0, s>>>(M, dna);
+    LAUNCH_CHECK();
+    HIP_TRY(hipMemcpyAsync(&na_h, dna, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipFreeAsync(dna, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (!na_h) plan->cell_flags |= FA_PLAN_AFFINE;
+  }
   plan->max_blocks = mb;
   plan->max_adj = ma;
   plan->slots = nullptr;
@@ -2859,12 +3017,13 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   using R = Rec<GD, NV, NQ, MAT>;
   // ordered (packed) slots are read only by the affine-simplex linear kernel of the same NSPLIT;
   // any other kernel searches its slots in LDS instead
-  if (P.slot_order && !((MAT == 0 || MAT == MAT_LINU) && R::SIMP && NN % NSPLIT == 0 && P.slot_order == NSPLIT)) {
+  if (P.slot_order && !((MAT == 0 || MAT == MAT_LINU || MAT == MAT_AFFT) && R::SIMP && NN % NSPLIT == 0 &&
+                        P.slot_order == NSPLIT)) {
     P.slots = nullptr;
     P.slot_order = 0;
     P.eadj = nullptr;
   }
-  static_assert(NN * GD <= 32, "bc mask holds 32 dofs");
+  static_assert(NN * GD <= 32 || MAT == MAT_AFFT, "bc mask holds 32 dofs");
   const int64_t nc = P.M.ncells;
   const int64_t rec_bytes = align256((int64_t)sizeof(double) * R::SIZE * nc);
   if (W.mode == GatherStage::SIZE) {
@@ -2892,6 +3051,11 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     if ((rc = chunk_desc(P, &desc, s))) return rc;
     const int64_t grid = gather_grid(k_gather<GD, NN, NV, NQ, NSPLIT, MAT>, P.nchunks);
     double* bhat = nullptr;
+    if constexpr (MAT == MAT_AFFT) {  // the kernel forms B_ab = r Ahat_ab + Ahat_ab^T per block
+      const double nu = P.F.nu;
+      P.rlm = 2.0 * nu / (1.0 - 2.0 * nu);
+      P.trc = 1.0 / (1.0 + P.rlm);
+    }
     if constexpr (MAT == MAT_LINU) {  // B_ab = r Ahat_ab + Ahat_ab^T for this form's nu
       const double nu = P.F.nu, rr = 2.0 * nu / (1.0 - 2.0 * nu);
       if ((rc = scratch_alloc((void**)&bhat, sizeof(double) * NN * NN * GD * GD, s))) return rc;
@@ -2996,6 +3160,18 @@ static bool lin_uniform_nu(const FormView& F) {
 static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const GatherArgs& P, const int8_t* bc,
                            hipStream_t s, bool* handled, const GatherStage& W = GatherStage()) {
   *handled = true;
+  if (m->cell_type == FA_HEXAHEDRON && kind == FA_LINEAR_ELASTICITY && P.affine && lin_uniform_nu(P.F)) {
+    // affine hexahedra: the row gather computes every block from the cell's Jacobian and the 1-D
+    // matrices (MAT_AFFT); the MFMA element kernel + block store serves general trilinear cells
+    if (m->degree == 1 && T.nq == 8) return launch_gather<3, 8, 8, 8, 2, MAT_AFFT>(P, bc, s, W);
+    if (m->degree == 2 && T.nq == 27) return launch_gather<3, 27, 8, 27, 9, MAT_AFFT>(P, bc, s, W);
+    if (m->degree == 3 && T.nq == 64) return launch_gather<3, 64, 8, 64, 32, MAT_AFFT>(P, bc, s, W);
+  }
+  if (m->cell_type == FA_QUADRILATERAL && kind == FA_LINEAR_ELASTICITY && P.affine && lin_uniform_nu(P.F)) {
+    if (m->degree == 1 && T.nq == 4) return launch_gather<2, 4, 4, 4, 1, MAT_AFFT>(P, bc, s, W);
+    if (m->degree == 2 && T.nq == 9) return launch_gather<2, 9, 4, 9, 3, MAT_AFFT>(P, bc, s, W);
+    if (m->degree == 3 && T.nq == 16) return launch_gather<2, 16, 4, 16, 4, MAT_AFFT>(P, bc, s, W);
+  }
   if (m->cell_type == FA_HEXAHEDRON && kind == FA_LINEAR_ELASTICITY) {
     if (m->degree == 1 && T.nq == 8) return launch_hex_gather<8, 8, 1>(P, T, bc, s, W);
     if (m->degree == 2 && T.nq == 27) return launch_hex_gather<27, 27, 3>(P, T, bc, s, W);
@@ -3103,6 +3279,8 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;
     P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr;
+    P.affine = (plan->cell_flags & FA_PLAN_AFFINE) != 0;
+    P.t1d = T.t1d; P.lat = T.lat;
     bool handled = false;
     rc = dispatch_gather(mesh, T, F.kind, P, bc, s, &handled);
     if (rc) return rc;
@@ -3157,6 +3335,8 @@ static int gather_stage(const fa_mesh* mesh, const fa_form* form, const fa_adjac
   P.M = M; P.F = F;
   P.A = BsrView{nullptr, nullptr, nullptr, 0, 0};
   P.tab = T.wq; P.ahat = T.ahat; P.bc = bc; P.diag = diag;
+  P.affine = 0;  // the prepare stage has no plan: tensor cells keep the element-kernel path
+  P.t1d = T.t1d; P.lat = T.lat;
   static int* derr = nullptr;  // device error word of the split path
   if (!derr) {
     HIP_TRY(hipMalloc((void**)&derr, sizeof(int)));

@@ -17,6 +17,7 @@ FA_OK = 0
 FA_TRIANGLE, FA_QUADRILATERAL, FA_TETRAHEDRON, FA_HEXAHEDRON = 3, 4, -4, 8
 FA_LINEAR_ELASTICITY, FA_ASYM_DAMAGE, FA_NEO_HOOKEAN = 0, 1, 2
 FA_GATHER, FA_SCATTER, FA_ZERO_FIRST = 0x0, 0x1, 0x2
+FA_PLAN_AFFINE = 0x1
 
 
 class FemasmError(RuntimeError):
@@ -79,7 +80,7 @@ class fa_plan(ctypes.Structure):
         ("max_adj", ctypes.c_int32),
         ("slots", ctypes.c_void_p),
         ("slot_order", ctypes.c_int32),
-        ("_pad", ctypes.c_int32),
+        ("cell_flags", ctypes.c_int32),
         ("eadj", ctypes.c_void_p),
     ]
 

@@ -106,6 +106,11 @@ typedef struct {
   const int32_t* idx;    /* [ncells*nn] flat dofmap positions p = cell*nn + local, sorted per node */
 } fa_adjacency;
 
+/* fa_plan.cell_flags */
+#define FA_PLAN_AFFINE 0x1   /* every cell of a tensor mesh is a parallelogram / parallelepiped: its
+                                hexahedra assemble through the affine row gather (no element-matrix
+                                store); otherwise through the MFMA element kernel + block gather */
+
 /* Row-chunk plan for the gather kernel (host-computed once per pattern). */
 typedef struct {
   int64_t nchunks;
@@ -116,7 +121,7 @@ typedef struct {
                                 node b, the block's position within row j's column list */
   int32_t slot_order;        /* 0: `slots` is that plain map; > 0: fa_plan_order rewrote it for the
                                 gather's item order (value = the kernel's column split) */
-  int32_t _pad;
+  int32_t cell_flags;        /* set by fa_plan_gather: FA_PLAN_AFFINE if every cell is affine */
   const int32_t* eadj;       /* positional plan (fa_plan_order with an entry buffer), else NULL:
                                 each chunk's adjacency entries in the plan's bank-balanced order;
                                 `slots` is then indexed by that position, chunk-relative */
