@@ -448,12 +448,14 @@ def main():
                          "unit": "TFLOP/s" if compute_bound else "GB/s",
                          "frac": round(fracs["flop_frac"] if compute_bound else fracs["frac"], 4), "traffic": traffic,
                          "hbm": {"achieved_GBps": round(achieved, 1), "frac": round(fracs["frac"], 4)},
-                         "fp64": {"flops_per_cell": f_e, "achieved_TFLOPs": round(tflops, 3),
-                                  "frac": round(fracs["flop_frac"], 4), "peak_TFLOPs": FP64_PEAK_TFLOPS,
-                                  "what": ("SURVEY §8(d) F_e (B^T D B contraction; AD passes not counted) "
-                                           "x cells / launch time") + ("" if compute_bound else
-                                          ": a model here -- the affine gathers form blocks from "
-                                          "reference tensors, not from the quadrature contraction")},
+                         ("fp64" if compute_bound else "model_fp64"): (
+                             {"flops_per_cell": f_e, "achieved_TFLOPs": round(tflops, 3),
+                              "frac": round(fracs["flop_frac"], 4), "peak_TFLOPs": FP64_PEAK_TFLOPS,
+                              "what": "SURVEY §8(d) F_e (B^T D B contraction; AD passes not counted) "
+                                      "x cells / launch time"} if compute_bound else
+                             {"flops_per_cell": f_e, "equivalent_TFLOPs": round(tflops, 3),
+                              "what": "SURVEY §8(d) F_e at this rate: the quadrature contraction's flops, "
+                                      "a model -- the gathers form blocks from reference tensors instead"}),
                          "traffic_GBps": None if traffic_gbps is None else round(traffic_gbps, 1),
                          "traffic_frac": None if traffic_gbps is None else round(fracs["traffic_frac"], 4),
                          "traffic_source": tsrc,

@@ -1353,8 +1353,13 @@ __device__ __forceinline__ int gather_perm(int jj, int na, int st, float inv) {
 #ifndef FA_BARY_WAVES
 #define FA_BARY_WAVES FA_GATHER_WAVES
 #endif
+#ifndef FA_NEOC_WAVES
+#define FA_NEOC_WAVES 3  // component neo-Hookean items keep a row of every column's block live (168 VGPRs)
+#endif
 template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT, int VAR = 0>
-__global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES : FA_GATHER_WAVES) void k_gather(GatherArgs P) {
+__global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES
+                                  : (MAT == FA_NEO_HOOKEAN && NSPLIT == GD ? FA_NEOC_WAVES : FA_GATHER_WAVES))
+void k_gather(GatherArgs P) {
   using R = Rec<GD, NV, NQ, MAT>;
   constexpr int BS2 = GD * GD;
   constexpr int MAXB = kGatherLdsValues / (8 * BS2);
@@ -1731,6 +1736,84 @@ __global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES : FA_GATHER_WAVES) vo
         bad |= s < 0;
         s = s < 0 ? MAXB : s;
         lds_add_block<2>(acc, s, K, (mask >> (aloc * 2)) & 3u, (mask >> (b * 2)) & 3u);
+      }
+    } else if constexpr (NEO && NSPLIT == GD) {
+      // Component items (NSPLIT = gdim): item (entry, i) computes row i of K_ab for ALL of the
+      // cell's columns b: per quadrature point C[k][L] = sum_J ga[J] A_q[(iJ)(kL)] (9 values from
+      // 27 tangent entries) once, then K_ab[i][k] += sum_L C[k][L] gb[L] for every b -- the
+      // contraction is shared by the NN columns instead of recomputed per column, and a record
+      // is read by GD items instead of NN.
+      constexpr int N = R::N;
+      const int ic = part;  // the output component of this item
+      const double* Aq0 = P.rec + c * R::SIZE + N + 1;
+      const double wdet = r[BS2];
+      int slb[NN];  // slots of all columns, loaded before the contraction (independent of it)
+#pragma unroll
+      for (int bb = 0; bb < NN; ++bb)
+        slb[bb] = P.slots ? lo + (int)P.slots[(a0 + j) * NN + bb] : lds_slot(cols, lo, hi, P.M.cells[c * NN + bb], niter);
+      double Kr[NN][GD];
+#pragma unroll
+      for (int bb = 0; bb < NN; ++bb)
+#pragma unroll
+        for (int k = 0; k < GD; ++k) Kr[bb][k] = 0.0;
+#pragma unroll 1
+      for (int q = 0; q < NQ; ++q) {
+        double ga[GD];
+#pragma unroll
+        for (int d = 0; d < GD; ++d) {
+          double sgd = 0.0;
+#pragma unroll
+          for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + aloc) * GD + k] * r[k * GD + d];
+          ga[d] = s_w[q] * wdet * sgd;
+        }
+        const double* Aq = Aq0 + q * R::NTRI;
+        double C[GD][GD];
+#pragma unroll
+        for (int k = 0; k < GD; ++k)
+#pragma unroll
+          for (int L = 0; L < GD; ++L) {
+            double t = 0.0;
+#pragma unroll
+            for (int J = 0; J < GD; ++J) {
+              const int row = ic * GD + J, col = k * GD + L;
+              // symmetric storage, upper triangle: row <= col ? (row, col) : (col, row)
+              const int ti = row <= col ? row * N - row * (row - 1) / 2 + (col - row) : col * N - col * (col - 1) / 2 + (row - col);
+              t = fma(ga[J], Aq[ti], t);
+            }
+            C[k][L] = t;
+          }
+#pragma unroll
+        for (int bb = 0; bb < NN; ++bb) {
+          double gb[GD];
+#pragma unroll
+          for (int d = 0; d < GD; ++d) {
+            double sgd = 0.0;
+#pragma unroll
+            for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + bb) * GD + k] * r[k * GD + d];
+            gb[d] = sgd;
+          }
+#pragma unroll
+          for (int k = 0; k < GD; ++k) {
+            double t = Kr[bb][k];
+#pragma unroll
+            for (int L = 0; L < GD; ++L) t = fma(C[k][L], gb[L], t);
+            Kr[bb][k] = t;
+          }
+          __builtin_amdgcn_sched_barrier(0);  // one column at a time: bounds the live table reads
+        }
+      }
+      // row dof (aloc, ic) constrained: the whole row of every block is zero; column dof (b, k): entry k
+      const bool rowc = (mask >> (aloc * GD + ic)) & 1u;
+#pragma unroll
+      for (int bb = 0; bb < NN; ++bb) {
+        int sb = slb[bb];
+        bad |= sb < 0;
+        sb = sb < 0 ? MAXB : sb;
+#pragma unroll
+        for (int k = 0; k < GD; ++k) {
+          const double v = (rowc || ((mask >> (bb * GD + k)) & 1u)) ? 0.0 : Kr[bb][k];
+          atomicAdd(&acc[sb * BS2 + ic * GD + k], v);
+        }
       }
     } else if constexpr (NEO) {
       // K_ab[i][k] = sum_q w_q |J| sum_{J,L} ga_q[J] A_q[(iJ)(kL)] gb_q[L]; per q the row node's
@@ -2485,7 +2568,8 @@ template <int NN, int NSPLIT>
 __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64_t* __restrict__ indptr,
                               const int64_t* __restrict__ adj_ptr, int64_t nchunks, int groups_per_chunk,
                               uint16_t* __restrict__ slots, const uint16_t* __restrict__ src,
-                              const uint16_t* __restrict__ eperm, unsigned long long* __restrict__ stats, int kicks) {
+                              const uint16_t* __restrict__ eperm, unsigned long long* __restrict__ stats, int kicks,
+                              int stats_rot) {
   constexpr int NBG = NN / NSPLIT, Q = 16;
   const int64_t total = nchunks * groups_per_chunk;
   for (int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gid < total;
@@ -2503,6 +2587,7 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
     const float inv = 1.0f / (float)na;
     const int nl = min(Q, nitems - p0);
     uint16_t off[Q][NBG];
+    uint16_t posv[Q][NBG];  // chunk-relative block position (stats only)
     uint8_t res[Q][NBG], pick[Q][NBG];
     uint8_t cnt[NBG][16];
     int64_t ent[Q];
@@ -2528,6 +2613,7 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
       ent[q] = (eperm ? a0 + p / NSPLIT : e) * NN + part * NBG;
       for (int t = 0; t < NBG; ++t) {
         off[q][t] = rd[ein + t];
+        posv[q][t] = (uint16_t)(rowlo + off[q][t]);
         res[q][t] = (uint8_t)((rowlo + off[q][t]) & 15);
         pick[q][t] = (uint8_t)t;
         ++cnt[t][res[q][t]];
@@ -2632,6 +2718,29 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
       atomicAdd(stats + 0, (unsigned long long)cost);
       atomicAdd(stats + 1, (unsigned long long)ident);
       atomicAdd(stats + 2, (unsigned long long)lb);
+      if (stats_rot) {
+        // measurement: passes of the 9 element instructions per step when block s's elements are
+        // stored rotated by (alpha s + beta) mod 9 (bank color (9 s + (k + rot) mod 9) mod 16),
+        // for every (alpha, beta); stats[3 + 9 alpha + beta], in instruction passes
+        for (int ab = 0; ab < 81; ++ab) {
+          const int al = ab / 9, be = ab % 9;
+          int c2 = 0;
+          for (int t = 0; t < NBG; ++t)
+            for (int k = 0; k < 9; ++k) {
+              uint8_t h[16];
+              for (int r = 0; r < 16; ++r) h[r] = 0;
+              int m = 0;
+              for (int q = 0; q < nl; ++q) {
+                const int sp = posv[q][pick[q][t]];
+                const int e = (k + (al * sp + be) % 9) % 9;
+                const int col = (9 * sp + e) & 15;
+                m = max(m, (int)++h[col]);
+              }
+              c2 += m;
+            }
+          atomicAdd(stats + 3 + ab, (unsigned long long)c2);
+        }
+      }
     }
     for (int q = 0; q < nl; ++q) {
       const int part = (p0 + q) % NSPLIT;
@@ -2702,6 +2811,95 @@ __global__ void k_plan_perm(const int64_t* __restrict__ row_start, const int64_t
   }
 }
 
+// Measurement (FA_ORDER_STATS=1c): how far a per-chunk XOR recolouring of the accumulator slots
+// (LDS position (s & ~15) | ((s & 15) ^ v_g), one 4-bit v per 16-block group g = s >> 4) flattens
+// each quarter's residue histogram. stats[84..86] += the pass bound sum over quarters before /
+// after (max(NBG, largest residue count)), quarters. One thread per chunk, positional plans.
+template <int NN, int NSPLIT>
+__global__ void k_plan_colors_stats(const int64_t* __restrict__ row_start, const int64_t* __restrict__ indptr,
+                                    const int64_t* __restrict__ adj_ptr, int64_t nchunks,
+                                    const uint16_t* __restrict__ src, const uint16_t* __restrict__ eperm,
+                                    unsigned long long* __restrict__ stats) {
+  constexpr int EQ = NSPLIT <= 16 ? 16 / NSPLIT : 1, NBG = NN / NSPLIT, MQ = kGatherMaxAdj / EQ, MG = 64;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r0 = row_start[c], r1 = row_start[c + 1];
+    const int64_t a0 = adj_ptr[r0];
+    const int na = (int)(adj_ptr[r1] - a0);
+    if (na <= 0) continue;
+    const int64_t b0 = indptr[r0];
+    const int nq = (na + EQ - 1) / EQ;
+    if (nq > 32) continue;
+    uint8_t cnt[32][16];
+    for (int q = 0; q < nq; ++q)
+      for (int r = 0; r < 16; ++r) cnt[q][r] = 0;
+    // hits per (group, quarter, low 4 bits): gh[g][q] bitmask is not enough (counts) -> per group
+    // a list of (quarter, low bits) hits
+    uint16_t hq[kGatherMaxAdj * NN];  // packed quarter << 8 | slot (slot < 512)
+    int nh = 0;
+    for (int pos = 0; pos < na; ++pos) {
+      const int j = (int)eperm[a0 + pos];
+      const int64_t e = a0 + j;
+      int64_t lo = r0, hi = r1 - 1;
+      while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (adj_ptr[mid] <= e) lo = mid; else hi = mid - 1;
+      }
+      const int rowlo = (int)(indptr[lo] - b0);
+      const int q = pos / EQ;
+      for (int b = 0; b < NN; ++b) {
+        const int sl = rowlo + src[e * NN + b];
+        hq[nh++] = (uint16_t)((q << 10) | sl);
+        ++cnt[q][sl & 15];
+      }
+    }
+    auto bound = [&]() {
+      int t = 0;
+      for (int q = 0; q < nq; ++q) {
+        int m = NBG;
+        for (int r = 0; r < 16; ++r) m = max(m, (int)cnt[q][r]);
+        t += m;
+      }
+      return t;
+    };
+    const int before = bound();
+    uint8_t v[MG];
+    for (int g = 0; g < MG; ++g) v[g] = 0;
+    for (int sweep = 0; sweep < 3; ++sweep) {
+      for (int g = 0; g < MG; ++g) {
+        // remove group g's hits, try the 16 XOR values, keep the one with the smallest sum of
+        // squared counts (ties: the current one)
+        bool any = false;
+        for (int k = 0; k < nh; ++k)
+          if (((hq[k] & 1023) >> 4) == g) {
+            any = true;
+            --cnt[hq[k] >> 10][(hq[k] & 15) ^ v[g]];
+          }
+        if (!any) continue;
+        int bestv = v[g];
+        long bestc = 1L << 60;
+        for (int x = 0; x < 16; ++x) {
+          long cst = 0;
+          for (int k = 0; k < nh; ++k)
+            if (((hq[k] & 1023) >> 4) == g) {
+              const int q = hq[k] >> 10, r = (hq[k] & 15) ^ x;
+              cst += 2 * cnt[q][r] + 1;  // increase of the sum of squares when adding this hit
+              ++cnt[q][r];
+            }
+          for (int k = 0; k < nh; ++k)
+            if (((hq[k] & 1023) >> 4) == g) --cnt[hq[k] >> 10][(hq[k] & 15) ^ x];
+          if (cst < bestc || (cst == bestc && x == v[g])) { bestc = cst; bestv = x; }
+        }
+        v[g] = (uint8_t)bestv;
+        for (int k = 0; k < nh; ++k)
+          if (((hq[k] & 1023) >> 4) == g) ++cnt[hq[k] >> 10][(hq[k] & 15) ^ v[g]];
+      }
+    }
+    atomicAdd(stats + 84, (unsigned long long)before);
+    atomicAdd(stats + 85, (unsigned long long)bound());
+    atomicAdd(stats + 86, (unsigned long long)nq);
+  }
+}
+
 // NSPLIT of the affine-simplex linear-elasticity gather kernel for (cell, degree, quadrature
 // points), or 0 when that kernel does not exist (must match dispatch_gather)
 #ifndef FA_P2TET_NSPLIT
@@ -2745,9 +2943,11 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   const char* ev = getenv("FA_ORDER_STATS");
   unsigned long long* st = nullptr;
   if (ev && ev[0] == '1') {
-    HIP_TRY(hipMallocAsync((void**)&st, 3 * sizeof(unsigned long long), s));
-    HIP_TRY(hipMemsetAsync(st, 0, 3 * sizeof(unsigned long long), s));
+    HIP_TRY(hipMallocAsync((void**)&st, 88 * sizeof(unsigned long long), s));
+    HIP_TRY(hipMemsetAsync(st, 0, 88 * sizeof(unsigned long long), s));
   }
+  const int stats_rot = (ev && ev[0] == '1' && ev[1] == 'r') ? 1 : 0;  // FA_ORDER_STATS=1r
+  const bool stats_col = ev && ev[0] == '1' && ev[1] == 'c';              // FA_ORDER_STATS=1c
   const char* ke = getenv("FEMASM_ORDER_KICKS");
   const int kicks = ke ? atoi(ke) : FA_ORDER_KICKS;
   // positional plan: the plain map is copied aside (the order kernel rewrites by position)
@@ -2764,8 +2964,12 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
     if (posn)                                                                                                 \
       k_plan_perm<NN_, NS_><<<grid_for(plan->nchunks), 64, 0, s>>>(plan->row_start, A->indptr, adj->ptr,      \
                                                                    adj->idx, plan->nchunks, src, eperm, eadj);   \
+    if (posn && stats_col)                                                                                    \
+      k_plan_colors_stats<NN_, NS_><<<grid_for(plan->nchunks, 64), 64, 0, s>>>(plan->row_start, A->indptr,        \
+                                                                              adj->ptr, plan->nchunks, src,     \
+                                                                              eperm, st);                       \
     k_order_slots<NN_, NS_><<<grid_for(total), 256, 0, s>>>(plan->row_start, A->indptr, adj->ptr, plan->nchunks, \
-                                                            groups, sl, src, eperm, st, kicks);               \
+                                                            groups, sl, src, eperm, st, kicks, stats_rot);    \
   } while (0)
   bool ok = true;
   if (mesh->nn == 3 && ns == 1) ORD(3, 1);
@@ -2790,12 +2994,24 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   }
   LAUNCH_CHECK();
   if (st) {
-    unsigned long long h[3];
+    unsigned long long h[88];
     HIP_TRY(hipMemcpyAsync(h, st, sizeof(h), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipFreeAsync(st, s));
     HIP_TRY(hipStreamSynchronize(s));
     fprintf(stderr, "fa_plan_order: LDS passes ordered %llu identity %llu bound %llu (%.3f / %.3f of identity)\n", h[0],
             h[1], h[2], (double)h[0] / (double)h[1], (double)h[2] / (double)h[1]);
+    if (stats_col)
+      fprintf(stderr, "fa_plan_order: XOR recolouring: pass bound per quarter %.3f -> %.3f (%llu quarters)\n",
+              (double)h[84] / (double)h[86], (double)h[85] / (double)h[86], h[86]);
+    if (stats_rot) {
+      int best = 0;
+      for (int ab = 1; ab < 81; ++ab)
+        if (h[3 + ab] < h[3 + best]) best = ab;
+      fprintf(stderr, "fa_plan_order: element-rotated passes: none %.4g, best global (alpha %d, beta %d) %.4g (%.3f)\n",
+              (double)h[3] / 9.0, best / 9, best % 9, (double)h[3 + best] / 9.0, (double)h[3 + best] / (double)h[3]);
+      for (int al = 0; al < 9; ++al)
+        fprintf(stderr, "  alpha %d: %.4f\n", al, (double)h[3 + 9 * al] / (double)h[3]);
+    }
   }
   HIP_TRY(hipStreamSynchronize(s));
   plan->slot_order = ns;
@@ -3105,7 +3321,8 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
 }
 
 #ifndef FA_NEO_NSPLIT
-#define FA_NEO_NSPLIT 10  // measured (n=120 sweep): 10 > 5 > 2
+#define FA_NEO_NSPLIT 10  // column items; 3 (= gdim) = component items sharing C over the columns: 576 vs 508 ms
+                          // on config E-neo (3 waves; 710 ms at 4) -- 3 items per entry leave the last item round idle
 #endif
 // Hexahedra: MFMA element blocks into a stream-ordered block store, then the row gather sums
 // them (the "store pass + per-destination sum pass" alternative to global atomics).
