@@ -901,6 +901,7 @@ struct GatherArgs {
   const int64_t* adj_ptr;
   const int32_t* adj_idx;
   const int64_t* row_start;
+  const int32_t* corder;   // [nchunks] visiting order (fa_plan_locality) or NULL (row order)
   const int64_t* chunk_b;  // [nchunks + 1] indptr[row_start[c]] (k_chunk_desc)
   const int64_t* chunk_a;  // [nchunks + 1] adj_ptr[row_start[c]]
   int64_t nchunks;
@@ -1356,9 +1357,18 @@ __device__ __forceinline__ int gather_perm(int jj, int na, int st, float inv) {
 #ifndef FA_NEOC_WAVES
 #define FA_NEOC_WAVES 3  // component neo-Hookean items keep a row of every column's block live (168 VGPRs)
 #endif
+// neo-Hookean column items: the per-q tangent (45 values) and C (27) are live together
+#ifndef FA_NEO_WAVES
+#define FA_NEO_WAVES 2  // 5 columns x (P, K) + a tangent sub-block live: 242 VGPRs, no spills in the item
+#endif
+// neo-Hookean P2-tet items by output component (VAR = 2): FA_NEO_COMPG column groups per
+// component, NSPLIT = gdim * groups (0: column items, NSPLIT = FA_NEO_NSPLIT)
+#ifndef FA_NEO_COMPG
+#define FA_NEO_COMPG 0
+#endif
 template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT, int VAR = 0>
 __global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES
-                                  : (MAT == FA_NEO_HOOKEAN && NSPLIT == GD ? FA_NEOC_WAVES : FA_GATHER_WAVES))
+                                  : (MAT == FA_NEO_HOOKEAN ? (VAR == 2 ? FA_NEOC_WAVES : FA_NEO_WAVES) : FA_GATHER_WAVES))
 void k_gather(GatherArgs P) {
   using R = Rec<GD, NV, NQ, MAT>;
   constexpr int BS2 = GD * GD;
@@ -1397,7 +1407,7 @@ void k_gather(GatherArgs P) {
   auto chunk_of = [&](int64_t v) -> int64_t {
     if (v >= 8 * per) return P.nchunks;
     const int64_t c = (v % 8) * per + v / 8;
-    return c < P.nchunks ? c : P.nchunks;
+    return c < P.nchunks ? (P.corder ? (int64_t)P.corder[c] : c) : P.nchunks;
   };
   // Chunk sequence of this workgroup. Static (P.ctr == NULL): chunk_of(blockIdx.x + k*gridDim.x).
   // Dynamic (persistent grid): lane 0 takes the next chunk of its XCD's range from a per-XCD
@@ -1424,7 +1434,10 @@ void k_gather(GatherArgs P) {
   };
   auto grab = [&]() -> int64_t {
     for (int t = 0; t < 9; ++t) {
-      if (s_bat[0] < s_bat[1]) return s_bat[0]++;
+      if (s_bat[0] < s_bat[1]) {
+        const int64_t v = s_bat[0]++;
+        return P.corder ? (int64_t)P.corder[v] : v;
+      }
       if (t == 8) break;
       const int q = (int)((blockIdx.x + t) & 7);
       if ((qdone >> q) & 1u) continue;
@@ -1737,23 +1750,29 @@ void k_gather(GatherArgs P) {
         s = s < 0 ? MAXB : s;
         lds_add_block<2>(acc, s, K, (mask >> (aloc * 2)) & 3u, (mask >> (b * 2)) & 3u);
       }
-    } else if constexpr (NEO && NSPLIT == GD) {
-      // Component items (NSPLIT = gdim): item (entry, i) computes row i of K_ab for ALL of the
-      // cell's columns b: per quadrature point C[k][L] = sum_J ga[J] A_q[(iJ)(kL)] (9 values from
-      // 27 tangent entries) once, then K_ab[i][k] += sum_L C[k][L] gb[L] for every b -- the
-      // contraction is shared by the NN columns instead of recomputed per column, and a record
-      // is read by GD items instead of NN.
+    } else if constexpr (NEO && VAR == 2) {
+      // Component items (VAR = 2, NSPLIT = gdim * G): item (entry, i, g) computes row i of K_ab for
+      // the g-th group of the cell's columns b: per quadrature point C[k][L] = sum_J ga[J]
+      // A_q[(iJ)(kL)] (9 values from 27 tangent entries) once, then K_ab[i][k] += sum_L C[k][L]
+      // gb[L] for every b of the group -- the contraction is shared by the group's columns instead
+      // of recomputed per column, and a record is read by gdim * G items instead of NN.
+      static_assert(NSPLIT % GD == 0, "component items: NSPLIT = gdim * groups");
+      constexpr int NG = NSPLIT / GD;            // column groups
+      constexpr int NC = (NN + NG - 1) / NG;     // columns per group
       constexpr int N = R::N;
-      const int ic = part;  // the output component of this item
+      const int ic = part % GD;  // the output component of this item
+      const int cb0 = (part / GD) * NC;  // its first column
       const double* Aq0 = P.rec + c * R::SIZE + N + 1;
       const double wdet = r[BS2];
-      int slb[NN];  // slots of all columns, loaded before the contraction (independent of it)
+      int slb[NC];  // slots of the group's columns, loaded before the contraction (independent of it)
 #pragma unroll
-      for (int bb = 0; bb < NN; ++bb)
-        slb[bb] = P.slots ? lo + (int)P.slots[(a0 + j) * NN + bb] : lds_slot(cols, lo, hi, P.M.cells[c * NN + bb], niter);
-      double Kr[NN][GD];
+      for (int bb = 0; bb < NC; ++bb) {
+        const int b = min(cb0 + bb, NN - 1);
+        slb[bb] = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_slot(cols, lo, hi, P.M.cells[c * NN + b], niter);
+      }
+      double Kr[NC][GD];
 #pragma unroll
-      for (int bb = 0; bb < NN; ++bb)
+      for (int bb = 0; bb < NC; ++bb)
 #pragma unroll
         for (int k = 0; k < GD; ++k) Kr[bb][k] = 0.0;
 #pragma unroll 1
@@ -1783,13 +1802,14 @@ void k_gather(GatherArgs P) {
             C[k][L] = t;
           }
 #pragma unroll
-        for (int bb = 0; bb < NN; ++bb) {
+        for (int bb = 0; bb < NC; ++bb) {
+          const int b = min(cb0 + bb, NN - 1);
           double gb[GD];
 #pragma unroll
           for (int d = 0; d < GD; ++d) {
             double sgd = 0.0;
 #pragma unroll
-            for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + bb) * GD + k] * r[k * GD + d];
+            for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + b) * GD + k] * r[k * GD + d];
             gb[d] = sgd;
           }
 #pragma unroll
@@ -1805,20 +1825,24 @@ void k_gather(GatherArgs P) {
       // row dof (aloc, ic) constrained: the whole row of every block is zero; column dof (b, k): entry k
       const bool rowc = (mask >> (aloc * GD + ic)) & 1u;
 #pragma unroll
-      for (int bb = 0; bb < NN; ++bb) {
+      for (int bb = 0; bb < NC; ++bb) {
+        const int b = cb0 + bb;
+        if (NN % NG != 0 && b >= NN) break;
         int sb = slb[bb];
         bad |= sb < 0;
         sb = sb < 0 ? MAXB : sb;
 #pragma unroll
         for (int k = 0; k < GD; ++k) {
-          const double v = (rowc || ((mask >> (bb * GD + k)) & 1u)) ? 0.0 : Kr[bb][k];
+          const double v = (rowc || ((mask >> (b * GD + k)) & 1u)) ? 0.0 : Kr[bb][k];
           atomicAdd(&acc[sb * BS2 + ic * GD + k], v);
         }
       }
     } else if constexpr (NEO) {
-      // K_ab[i][k] = sum_q w_q |J| sum_{J,L} ga_q[J] A_q[(iJ)(kL)] gb_q[L]; per q the row node's
-      // gradient is contracted first, C[i][k][L] = sum_J ga[J] A[(iJ)(kL)] (compile-time indices,
-      // each tangent entry loaded once per item), then applied to every column node.
+      // K_ab[i][k] = sum_q sum_{J,L} P[J][L] A_q[(iJ)(kL)] with P = (w_q |J| ga) (x) gb: the outer
+      // product first, then each 3x3 sub-block A_ik of the symmetric tangent is read once and serves
+      // K[i][k] and K[k][i] (K[k][i] = sum P[L][J] A_ik[J][L]). Only P, K and one sub-block are live,
+      // where contracting the row gradient first (C[i][k][L], 27 values) held C and all 45 tangent
+      // values at once and spilled (133 VGPRs at 4 waves / SIMD).
       constexpr int N = R::N;
       const double* Aq0 = P.rec + c * R::SIZE + N + 1;
       const double wdet = r[BS2];
@@ -1840,25 +1864,10 @@ void k_gather(GatherArgs P) {
           ga[d] = s_w[q] * wdet * sgd;
         }
         const double* Aq = Aq0 + q * R::NTRI;
-        double C[GD][GD][GD];
-#pragma unroll
-        for (int i = 0; i < GD; ++i)
-#pragma unroll
-          for (int k = 0; k < GD; ++k)
-#pragma unroll
-            for (int L = 0; L < GD; ++L) {
-              double t = 0.0;
-#pragma unroll
-              for (int J = 0; J < GD; ++J) {
-                const int row = i * GD + J, col = k * GD + L;
-                t += ga[J] * Aq[row <= col ? tri_index(row, col, N) : tri_index(col, row, N)];
-              }
-              C[i][k][L] = t;
-            }
+        double Pm[NBG][GD][GD];  // (w |J| ga) (x) gb per column node of the item
 #pragma unroll
         for (int bb = 0; bb < NBG; ++bb) {
-          const int b = part * NBG + bb;
-          if (b >= NN) break;
+          const int b = min(part * NBG + bb, NN - 1);  // past-the-end columns: computed, never added
           double gb[GD];
 #pragma unroll
           for (int d = 0; d < GD; ++d) {
@@ -1868,14 +1877,52 @@ void k_gather(GatherArgs P) {
             gb[d] = sgd;
           }
 #pragma unroll
-          for (int i = 0; i < GD; ++i)
+          for (int J = 0; J < GD; ++J)
 #pragma unroll
-            for (int k = 0; k < GD; ++k) {
-              double t = 0.0;
+            for (int L = 0; L < GD; ++L) Pm[bb][J][L] = ga[J] * gb[L];
+        }
+        // each sub-block of the tangent is loaded once and applied to every column of the item
 #pragma unroll
-              for (int L = 0; L < GD; ++L) t += C[i][k][L] * gb[L];
-              K[bb][i][k] += t;
+        for (int i = 0; i < GD; ++i) {
+          {  // diagonal sub-block: symmetric in (J, L)
+            double Ad[GD][GD];
+#pragma unroll
+            for (int J = 0; J < GD; ++J)
+#pragma unroll
+              for (int L = J; L < GD; ++L) Ad[J][L] = Aq[tri_index(i * GD + J, i * GD + L, N)];
+#pragma unroll
+            for (int bb = 0; bb < NBG; ++bb) {
+              double t = K[bb][i][i];
+#pragma unroll
+              for (int J = 0; J < GD; ++J) {
+                t = fma(Pm[bb][J][J], Ad[J][J], t);
+#pragma unroll
+                for (int L = J + 1; L < GD; ++L) t = fma(Pm[bb][J][L] + Pm[bb][L][J], Ad[J][L], t);
+              }
+              K[bb][i][i] = t;
             }
+          }
+#pragma unroll
+          for (int k = i + 1; k < GD; ++k) {
+            double Ao[GD][GD];
+#pragma unroll
+            for (int J = 0; J < GD; ++J)
+#pragma unroll
+              for (int L = 0; L < GD; ++L) Ao[J][L] = Aq[tri_index(i * GD + J, k * GD + L, N)];
+#pragma unroll
+            for (int bb = 0; bb < NBG; ++bb) {
+              double t1 = K[bb][i][k], t2 = K[bb][k][i];
+#pragma unroll
+              for (int J = 0; J < GD; ++J)
+#pragma unroll
+                for (int L = 0; L < GD; ++L) {
+                  t1 = fma(Pm[bb][J][L], Ao[J][L], t1);
+                  t2 = fma(Pm[bb][L][J], Ao[J][L], t2);
+                }
+              K[bb][i][k] = t1;
+              K[bb][k][i] = t2;
+            }
+          }
         }
       }
 #pragma unroll
@@ -3110,6 +3157,124 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
   plan->slots = nullptr;
   plan->slot_order = 0;
   plan->eadj = nullptr;
+  plan->corder = nullptr;
+  return FA_OK;
+}
+
+// ------------------------------------------------------------------------------- chunk locality order
+static int scratch_alloc(void** p, size_t bytes, hipStream_t s);
+static inline int64_t align256(int64_t b);
+// Doubles <-> order-preserving unsigned keys (for atomic min / max of coordinates).
+__device__ inline unsigned long long ordered_key(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+__device__ inline double ordered_val(unsigned long long k) {
+  return __longlong_as_double((long long)((k >> 63) ? (k & ~(1ull << 63)) : ~k));
+}
+// a point per chunk: the centroid of the cell of the chunk's first adjacency entry; bounding box
+// of the points in bb[0..2] (min keys) / bb[3..5] (max keys), one atomic per workgroup and axis
+__global__ __launch_bounds__(256) void k_chunk_points(MeshView M, const int64_t* __restrict__ row_start, int64_t nchunks,
+                                                      const int64_t* __restrict__ adj_ptr,
+                                                      const int32_t* __restrict__ adj_idx, double* __restrict__ pts,
+                                                      unsigned long long* __restrict__ bb) {
+  __shared__ unsigned long long smin[3][256], smax[3][256];
+  unsigned long long lmin[3] = {~0ull, ~0ull, ~0ull}, lmax[3] = {0ull, 0ull, 0ull};
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nchunks; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = adj_ptr[row_start[k]];
+    const int64_t c = adj_idx[e] / M.nn;
+    double p[3] = {0.0, 0.0, 0.0};
+    for (int v = 0; v < M.nv; ++v)
+      for (int i = 0; i < M.gd; ++i) p[i] += M.x[(int64_t)M.geom[c * M.nv + v] * M.gd + i];
+    for (int i = 0; i < 3; ++i) {
+      p[i] /= (double)M.nv;
+      pts[k * 3 + i] = p[i];
+      const unsigned long long q = ordered_key(p[i]);
+      lmin[i] = min(lmin[i], q);
+      lmax[i] = max(lmax[i], q);
+    }
+  }
+  for (int i = 0; i < 3; ++i) {
+    smin[i][threadIdx.x] = lmin[i];
+    smax[i][threadIdx.x] = lmax[i];
+  }
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w)
+      for (int i = 0; i < 3; ++i) {
+        smin[i][threadIdx.x] = min(smin[i][threadIdx.x], smin[i][threadIdx.x + w]);
+        smax[i][threadIdx.x] = max(smax[i][threadIdx.x], smax[i][threadIdx.x + w]);
+      }
+    __syncthreads();
+  }
+  if (threadIdx.x < 3) {
+    atomicMin(bb + threadIdx.x, smin[threadIdx.x][0]);
+    atomicMax(bb + 3 + threadIdx.x, smax[threadIdx.x][0]);
+  }
+}
+__device__ inline uint64_t spread3(uint64_t v) {  // 21 bits -> every third bit
+  v &= 0x1fffffull;
+  v = (v | (v << 32)) & 0x1f00000000ffffull;
+  v = (v | (v << 16)) & 0x1f0000ff0000ffull;
+  v = (v | (v << 8)) & 0x100f00f00f00f00full;
+  v = (v | (v << 4)) & 0x10c30c30c30c30c3ull;
+  v = (v | (v << 2)) & 0x1249249249249249ull;
+  return v;
+}
+__global__ void k_chunk_morton(const double* __restrict__ pts, int64_t nchunks, const unsigned long long* __restrict__ bb,
+                               uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nchunks; k += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t key = 0;
+    for (int i = 0; i < 3; ++i) {
+      const double lo = ordered_val(bb[i]), hi = ordered_val(bb[3 + i]);
+      const double t = hi > lo ? (pts[k * 3 + i] - lo) / (hi - lo) : 0.0;
+      const uint64_t q = (uint64_t)fmin(fmax(t * 2097152.0, 0.0), 2097151.0);
+      key |= spread3(q) << i;
+    }
+    keys[k] = key;
+    vals[k] = (int32_t)k;
+  }
+}
+
+extern "C" int fa_plan_locality(const fa_mesh* mesh, const fa_adjacency* adj, int32_t* corder, fa_plan* plan,
+                                void* stream) {
+  int rc = check_mesh(mesh);
+  if (rc) return rc;
+  if (!adj || !adj->ptr || !adj->idx || !corder || !plan || !plan->row_start) return fail(FA_E_ARG, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = plan->nchunks;
+  if (n >= (1ll << 31)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks (>= 2^31)", (long long)n);
+  if (n <= 1 || mesh->ncells == 0) {
+    plan->corder = nullptr;
+    return FA_OK;
+  }
+  MeshView M{mesh->cells, mesh->geom, mesh->x, mesh->ncells, mesh->nnodes, mesh->nn, mesh->nv, mesh->gdim};
+  // scratch: points [n][3] f64, bbox 6 keys, keys in/out u64, vals in i32, radix-sort temp
+  size_t temp_bytes = 0;
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                             (int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 63, s));
+  const size_t off_bb = align256(sizeof(double) * 3 * n);
+  const size_t off_k0 = off_bb + 256;
+  const size_t off_k1 = off_k0 + align256(sizeof(uint64_t) * n);
+  const size_t off_v = off_k1 + align256(sizeof(uint64_t) * n);
+  const size_t off_t = off_v + align256(sizeof(int32_t) * n);
+  char* buf = nullptr;
+  if ((rc = scratch_alloc((void**)&buf, off_t + temp_bytes, s))) return rc;
+  double* pts = reinterpret_cast<double*>(buf);
+  unsigned long long* bb = reinterpret_cast<unsigned long long*>(buf + off_bb);
+  uint64_t* k0 = reinterpret_cast<uint64_t*>(buf + off_k0);
+  uint64_t* k1 = reinterpret_cast<uint64_t*>(buf + off_k1);
+  int32_t* v0 = reinterpret_cast<int32_t*>(buf + off_v);
+  const unsigned long long init[6] = {~0ull, ~0ull, ~0ull, 0ull, 0ull, 0ull};
+  HIP_TRY(hipMemcpyAsync(bb, init, sizeof(init), hipMemcpyHostToDevice, s));
+  k_chunk_points<<<grid_for(n), 256, 0, s>>>(M, plan->row_start, n, adj->ptr, adj->idx, pts, bb);
+  LAUNCH_CHECK();
+  k_chunk_morton<<<grid_for(n), 256, 0, s>>>(pts, n, bb, k0, v0);
+  LAUNCH_CHECK();
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(buf + off_t, temp_bytes, k0, k1, v0, corder, (int)n, 0, 63, s));
+  HIP_TRY(hipFreeAsync(buf, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  plan->corder = corder;
   return FA_OK;
 }
 
@@ -3228,7 +3393,7 @@ __global__ void k_bhat(const double* __restrict__ ahat, int nblk, double r, doub
         bhat[t * GD * GD + i * GD + k] = r * ahat[t * GD * GD + i * GD + k] + ahat[t * GD * GD + k * GD + i];
 }
 
-template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT>
+template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT, int VAR = 0>
 static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const GatherStage& W) {
   using R = Rec<GD, NV, NQ, MAT>;
   // ordered (packed) slots are read only by the affine-simplex linear kernel of the same NSPLIT;
@@ -3265,7 +3430,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   if (P.nchunks > 0 && W.mode != GatherStage::PREP) {
     int64_t* desc = nullptr;
     if ((rc = chunk_desc(P, &desc, s))) return rc;
-    const int64_t grid = gather_grid(k_gather<GD, NN, NV, NQ, NSPLIT, MAT>, P.nchunks);
+    const int64_t grid = gather_grid(k_gather<GD, NN, NV, NQ, NSPLIT, MAT, VAR>, P.nchunks);
     double* bhat = nullptr;
     if constexpr (MAT == MAT_AFFT) {  // the kernel forms B_ab = r Ahat_ab + Ahat_ab^T per block
       const double nu = P.F.nu;
@@ -3296,7 +3461,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
         launched = true;
       }
     }
-    if (!launched) k_gather<GD, NN, NV, NQ, NSPLIT, MAT><<<(unsigned)grid, 256, 0, s>>>(P);
+    if (!launched) k_gather<GD, NN, NV, NQ, NSPLIT, MAT, VAR><<<(unsigned)grid, 256, 0, s>>>(P);
     LAUNCH_CHECK();
 #if FA_GATHER_TIMING
     {
@@ -3321,8 +3486,8 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
 }
 
 #ifndef FA_NEO_NSPLIT
-#define FA_NEO_NSPLIT 10  // column items; 3 (= gdim) = component items sharing C over the columns: 576 vs 508 ms
-                          // on config E-neo (3 waves; 710 ms at 4) -- 3 items per entry leave the last item round idle
+#define FA_NEO_NSPLIT 2  // column items of 5 columns sharing each tangent sub-block load; config E-neo at
+                         // 2 waves / SIMD: 342 ms (NSPLIT 5 at 3 waves 349, 10 at 4 waves 461)
 #endif
 // Hexahedra: MFMA element blocks into a stream-ordered block store, then the row gather sums
 // them (the "store pass + per-destination sum pass" alternative to global atomics).
@@ -3397,7 +3562,13 @@ static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const
   const int ct = m->cell_type, p = m->degree, nq = T.nq;
   if (kind == FA_ASYM_DAMAGE) return launch_gather<2, 3, 3, 1, 1, FA_ASYM_DAMAGE>(P, bc, s, W);
   if (kind == FA_NEO_HOOKEAN) {
-    if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, FA_NEO_NSPLIT, FA_NEO_HOOKEAN>(P, bc, s, W);
+    if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) {
+#if FA_NEO_COMPG > 0
+      return launch_gather<3, 10, 4, 4, 3 * FA_NEO_COMPG, FA_NEO_HOOKEAN, 2>(P, bc, s, W);
+#else
+      return launch_gather<3, 10, 4, 4, FA_NEO_NSPLIT, FA_NEO_HOOKEAN>(P, bc, s, W);
+#endif
+    }
     if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, FA_NEO_HOOKEAN>(P, bc, s, W);
     if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, FA_NEO_HOOKEAN>(P, bc, s, W);
     if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, FA_NEO_HOOKEAN>(P, bc, s, W);
@@ -3491,7 +3662,7 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
       return fail(FA_E_ARG, "FA_GATHER needs the adjacency and a plan (fa_plan_gather)");
     GatherArgs P;
     P.M = M; P.F = F; P.A = Av;
-    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks;
+    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks; P.corder = plan->corder;
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;
@@ -3569,7 +3740,7 @@ static int gather_stage(const fa_mesh* mesh, const fa_form* form, const fa_adjac
     if (!adj || !adj->ptr || !adj->idx || !plan || !plan->row_start)
       return fail(FA_E_ARG, "fa_gather_rows needs the adjacency and a plan (fa_plan_gather)");
     P.A = BsrView{A->indptr, A->indices, A->data, wb, we};
-    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks;
+    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks; P.corder = plan->corder;
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;

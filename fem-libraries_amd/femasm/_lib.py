@@ -82,6 +82,7 @@ class fa_plan(ctypes.Structure):
         ("slot_order", ctypes.c_int32),
         ("cell_flags", ctypes.c_int32),
         ("eadj", ctypes.c_void_p),
+        ("corder", ctypes.c_void_p),
     ]
 
 
@@ -98,6 +99,7 @@ SIGNATURES = {
     "fa_plan_gather": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_plan_slots": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_plan_order": (ctypes.c_int, [P, P, P, P, P, P]),
+    "fa_plan_locality": (ctypes.c_int, [P, P, P, P, P]),
     "fa_tabulate_cells": (ctypes.c_int, [P, P, I64, I64, P, P]),
     "fa_assemble_matrix": (ctypes.c_int, [P, P, P, P, P, D, P, I32, P]),
     "fa_gather_work_bytes": (ctypes.c_int, [P, P, P]),

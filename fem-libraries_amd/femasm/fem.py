@@ -496,6 +496,18 @@ def _plan_order(V, fm, adj, fb, plan, sh, eadj=None):
     return eadj if plan.eadj else None
 
 
+def _plan_locality(V, fm, adj, plan, sh):
+    """Chunk visiting order of the gather (fa_plan_locality): Morton order of the chunks' positions,
+    so chunks that share cells run close in time and the cells' records are re-read from L2, not
+    HBM. FEMASM_CHUNK_ORDER=0 keeps row order."""
+    if os.environ.get("FEMASM_CHUNK_ORDER", "morton") == "0" or plan.nchunks <= 1:
+        return None
+    corder = torch.empty(plan.nchunks, dtype=torch.int32, device=V.mesh.device)
+    _lib.check(_lib.load().fa_plan_locality(ctypes.byref(fm), ctypes.byref(adj), corder.data_ptr(),
+                                            ctypes.byref(plan), sh), "fa_plan_locality")
+    return corder if plan.corder else None
+
+
 def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0):
     """Row-chunk plan of the gather kernel for one row part of A's pattern (cached on V)."""
     plans = V.__dict__.setdefault("_plans", {})
@@ -521,7 +533,8 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0):
             _lib.check(L.fa_plan_slots(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), slots.data_ptr(),
                                        ctypes.byref(plan), sh), "fa_plan_slots")
             eadj = _plan_order(V, fm, adj, fb, plan, sh)
-        plans[key] = (plan, rs, A.indptr, slots, eadj)
+        corder = _plan_locality(V, fm, adj, plan, sh)
+        plans[key] = (plan, rs, A.indptr, slots, eadj, corder)
     return plans[key][0]
 
 
@@ -597,6 +610,8 @@ class SplitGather:
             self.subs.append(fb)
             self.plans.append(plan)
             self._keep.append(rs)
+            if r1 > r0:
+                self._keep.append(_plan_locality(V, self.fm, self.adj, plan, self.sh))
         if self.slots is not None:
             # one slot map for all rows (fa_plan_slots writes every row), then each plan's order
             live = [i for i, (r0, r1) in enumerate(ranges) if r1 > r0]

@@ -125,6 +125,8 @@ typedef struct {
   const int32_t* eadj;       /* positional plan (fa_plan_order with an entry buffer), else NULL:
                                 each chunk's adjacency entries in the plan's bank-balanced order;
                                 `slots` is then indexed by that position, chunk-relative */
+  const int32_t* corder;     /* optional device [nchunks] (fa_plan_locality): the order in which the
+                                gather visits its chunks; NULL = row order */
 } fa_plan;
 
 const char* fa_last_error(void);
@@ -166,6 +168,13 @@ int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A,
  * rewrites all rows). */
 int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int32_t* eadj, fa_plan* plan,
                   void* stream);
+
+/* Chunk visiting order for cache locality: chunks sorted by the Morton key of a point of each
+ * chunk (the centroid of the cell of its first adjacency entry), so that chunks the gather runs
+ * close in time share cells and their per-cell records stay in L2. corder is a caller-owned device
+ * buffer of plan->nchunks int32; on success plan->corder points to it. Any permutation assembles
+ * the same matrix (each chunk owns its rows); only the re-reads of the records change. */
+int fa_plan_locality(const fa_mesh* mesh, const fa_adjacency* adj, int32_t* corder, fa_plan* plan, void* stream);
 
 /* Per-cell element matrices Ae [ncells_out][nn*bs][nn*bs] (dof = node*bs + comp) for cells
  * [c0, c0+ncells_out) — the batched ufcx tabulate_tensor / AssembleElementGrad. */

@@ -93,3 +93,25 @@ def test_slot_order(dev, oracle, monkeypatch, order, ct, p, n):
     torch.cuda.synchronize()
     err = np.abs(A.data.cpu().numpy() - ref).max() / np.abs(ref).max()
     assert err <= RTOL, err
+
+
+@pytest.mark.parametrize("order", ["morton", "0"])
+@pytest.mark.parametrize("ct,p,n", [("tetrahedron", 2, 5), ("hexahedron", 2, 4), ("triangle", 1, 12)])
+def test_chunk_locality_order(dev, oracle, monkeypatch, order, ct, p, n):
+    """fa_plan_locality: the gather visits its chunks in Morton order of their positions (default) or
+    in row order (FEMASM_CHUNK_ORDER=0); the order is a permutation and the matrix is the oracle's."""
+    from femasm import fem
+
+    monkeypatch.setenv("FEMASM_CHUNK_ORDER", order)
+    V, a, bcs, indptr, indices, ref = _problem(dev, oracle, ct, p, n)
+    A = fem.assemble_matrix(a, bcs=bcs)
+    entry = next(iter(V.__dict__["_plans"].values()))
+    plan, corder = entry[0], entry[5]
+    if order == "0" or plan.nchunks <= 1:
+        assert corder is None and not plan.corder
+    else:
+        assert plan.corder == corder.data_ptr()
+        assert torch.equal(torch.sort(corder.cpu()).values, torch.arange(plan.nchunks, dtype=torch.int32))
+    torch.cuda.synchronize()
+    err = np.abs(A.data.cpu().numpy() - ref).max() / np.abs(ref).max()
+    assert err <= RTOL, err

@@ -5,7 +5,7 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 if [ "${PARITY:-0}" = 1 ]; then
-  env ${PARITY_ENV:-X=1} timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_linu.py tests/test_gpu_split.py -x -q \
+  env ${PARITY_ENV:-X=1} timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_linu.py tests/test_gpu_split.py tests/test_gpu_neohookean.py -x -q \
     --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_quick.log 2>&1
   rc=$?; tail -2 gpurun_out/pytest_quick.log; [ $rc -eq 0 ] || exit $rc
 fi
