@@ -1864,63 +1864,62 @@ void k_gather(GatherArgs P) {
           ga[d] = s_w[q] * wdet * sgd;
         }
         const double* Aq = Aq0 + q * R::NTRI;
-        double Pm[NBG][GD][GD];  // (w |J| ga) (x) gb per column node of the item
+        double gb[NBG][GD];  // column gradients of the item
 #pragma unroll
         for (int bb = 0; bb < NBG; ++bb) {
           const int b = min(part * NBG + bb, NN - 1);  // past-the-end columns: computed, never added
-          double gb[GD];
 #pragma unroll
           for (int d = 0; d < GD; ++d) {
             double sgd = 0.0;
 #pragma unroll
             for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + b) * GD + k] * r[k * GD + d];
-            gb[d] = sgd;
+            gb[bb][d] = sgd;
           }
-#pragma unroll
-          for (int J = 0; J < GD; ++J)
-#pragma unroll
-            for (int L = 0; L < GD; ++L) Pm[bb][J][L] = ga[J] * gb[L];
         }
-        // each sub-block of the tangent is loaded once and applied to every column of the item
+        // per 3x3 sub-block A_ik of the tangent (loaded once per item): the row gradient is
+        // contracted first, C[L] = sum_J ga[J] A_ik[J][L] (and C'[L] = sum_J ga[J] A_ik[L][J] for
+        // K[k][i]), then C is applied to every column: 81 + 27 NBG FMAs per point, and only ga, the
+        // columns' gb and K, one sub-block and C live
 #pragma unroll
         for (int i = 0; i < GD; ++i) {
-          {  // diagonal sub-block: symmetric in (J, L)
-            double Ad[GD][GD];
+#pragma unroll
+          for (int k = i; k < GD; ++k) {
+            double Ab[GD][GD];
 #pragma unroll
             for (int J = 0; J < GD; ++J)
 #pragma unroll
-              for (int L = J; L < GD; ++L) Ad[J][L] = Aq[tri_index(i * GD + J, i * GD + L, N)];
-#pragma unroll
-            for (int bb = 0; bb < NBG; ++bb) {
-              double t = K[bb][i][i];
-#pragma unroll
-              for (int J = 0; J < GD; ++J) {
-                t = fma(Pm[bb][J][J], Ad[J][J], t);
-#pragma unroll
-                for (int L = J + 1; L < GD; ++L) t = fma(Pm[bb][J][L] + Pm[bb][L][J], Ad[J][L], t);
-              }
-              K[bb][i][i] = t;
-            }
-          }
-#pragma unroll
-          for (int k = i + 1; k < GD; ++k) {
-            double Ao[GD][GD];
-#pragma unroll
-            for (int J = 0; J < GD; ++J)
-#pragma unroll
-              for (int L = 0; L < GD; ++L) Ao[J][L] = Aq[tri_index(i * GD + J, k * GD + L, N)];
-#pragma unroll
-            for (int bb = 0; bb < NBG; ++bb) {
-              double t1 = K[bb][i][k], t2 = K[bb][k][i];
+              for (int L = 0; L < GD; ++L)
+                Ab[J][L] = (i == k && L < J) ? 0.0 : Aq[tri_index(i * GD + J, k * GD + L, N)];
+            if (i == k) {
 #pragma unroll
               for (int J = 0; J < GD; ++J)
 #pragma unroll
-                for (int L = 0; L < GD; ++L) {
-                  t1 = fma(Pm[bb][J][L], Ao[J][L], t1);
-                  t2 = fma(Pm[bb][L][J], Ao[J][L], t2);
-                }
+                for (int L = 0; L < J; ++L) Ab[J][L] = Ab[L][J];  // symmetric diagonal sub-block
+            }
+            double C[GD], Ct[GD];
+#pragma unroll
+            for (int L = 0; L < GD; ++L) {
+              double t = 0.0, u = 0.0;
+#pragma unroll
+              for (int J = 0; J < GD; ++J) {
+                t = fma(ga[J], Ab[J][L], t);
+                if (i != k) u = fma(ga[J], Ab[L][J], u);
+              }
+              C[L] = t;
+              Ct[L] = u;
+            }
+#pragma unroll
+            for (int bb = 0; bb < NBG; ++bb) {
+              double t1 = K[bb][i][k];
+#pragma unroll
+              for (int L = 0; L < GD; ++L) t1 = fma(C[L], gb[bb][L], t1);
               K[bb][i][k] = t1;
-              K[bb][k][i] = t2;
+              if (i != k) {
+                double t2 = K[bb][k][i];
+#pragma unroll
+                for (int L = 0; L < GD; ++L) t2 = fma(Ct[L], gb[bb][L], t2);
+                K[bb][k][i] = t2;
+              }
             }
           }
         }
