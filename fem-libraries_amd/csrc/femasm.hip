@@ -950,7 +950,12 @@ __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, co
       double Fq[N];
       deformation_gradient<GD>(F.u, cn, NN, tab + NQ + q * NN * GD, Ji, Fq);
       using DD = Dual<Dual<double>>;
+      // the n(n+1)/2 hyper-dual passes unrolled: with compile-time one-hot seeds the compiler drops
+      // the zero derivative terms and evaluates the primal parts (F:F, det F, its log and inverse)
+      // once for all passes instead of once per pass
+#pragma unroll
       for (int i = 0; i < N; ++i)
+#pragma unroll
         for (int j = i; j < N; ++j) {
           DD x[N];
 #pragma unroll
@@ -1627,8 +1632,9 @@ void k_gather(GatherArgs P) {
   if (IPF && nchunk < P.nchunks) {
     const int na_n = (int)(nxt.a1 - nxt.a0);
     if (tid < na_n * NSPLIT) {
-      pj_n = perm(tid / NSPLIT, na_n, perm_stride(na_n), 1.0f / (float)na_n);
-      pflat_n = P.adj_idx[nxt.a0 + pj_n];
+      // positional plan: entries in the plan's order, item it -> position it / NSPLIT
+      pj_n = (POSM && P.eadj != nullptr) ? tid / NSPLIT : perm(tid / NSPLIT, na_n, perm_stride(na_n), 1.0f / (float)na_n);
+      pflat_n = adj_src[nxt.a0 + pj_n];
     }
   }
   Desc nn2;  // chunk k+2's descriptor: loaded after the items (scalar loads), used from the next chunk on
@@ -1957,9 +1963,18 @@ void k_gather(GatherArgs P) {
       uint64_t bcp = 0;
 #pragma unroll
       for (int bb = 0; bb < NBG; ++bb) bcp |= (uint64_t)(part * NBG + bb) << (6 * bb);
-      if (decltype(FROMPF)::value && P.slots) {  // prefetched slot offsets
+      if (decltype(FROMPF)::value && P.slots) {  // prefetched slot map entries
+        if (P.slot_order) {  // (b << 10) | position
 #pragma unroll
-        for (int bb = 0; bb < NBG; ++bb) sl[bb] = lo + cn[bb];
+          for (int bb = 0; bb < NBG; ++bb) {
+            const int v = cn[bb];
+            sl[bb] = lo + (v & 1023);
+            bcp = (bcp & ~((uint64_t)63 << (6 * bb))) | ((uint64_t)(v >> 10) << (6 * bb));
+          }
+        } else {
+#pragma unroll
+          for (int bb = 0; bb < NBG; ++bb) sl[bb] = lo + cn[bb];
+        }
       } else if (P.slots && P.slot_order) {  // (b << 10) | position, in bank-conflict-aware order
 #pragma unroll
         for (int bb = 0; bb < NBG; ++bb) {
@@ -2198,7 +2213,7 @@ void k_gather(GatherArgs P) {
   if (abl_sink == 1.2345) acc[0] = abl_sink;
 #endif
   have_pf = false;
-  if (IPF && nchunk < P.nchunks && !P.slot_order) {
+  if (IPF && nchunk < P.nchunks) {
     have_pf = true;
     const int na_n = (int)(nxt.a1 - nxt.a0);
     if (tid < na_n * NSPLIT) {
@@ -2215,7 +2230,7 @@ void k_gather(GatherArgs P) {
 #pragma unroll
         for (int bb = 0; bb < NBG; ++bb) {
           const int b = part * NBG + bb;
-          pcn[bb] = b < NN ? (int32_t)P.slots[(nxt.a0 + pj_n) * NN + b] : 0;
+          pcn[bb] = b < NN ? (int32_t)P.slots[((int64_t)nxt.a0 + pj_n) * NN + b] : 0;
         }
       } else {
 #pragma unroll
@@ -3404,6 +3419,13 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     P.eadj = nullptr;
   }
   static_assert(NN * GD <= 32 || MAT == MAT_AFFT, "bc mask holds 32 dofs");
+  // locality order: pays where the records are large (neo-Hookean tangents, 1.5 KB per cell:
+  // 342 -> 328 ms on config E-neo); the 80-B linear records stay in L2 in row order (E: 50.0 vs
+  // 51.5 ms in Morton order). FEMASM_CHUNK_ORDER_ALL=1 applies it to every kernel.
+  {
+    const char* e = getenv("FEMASM_CHUNK_ORDER_ALL");
+    if (MAT != FA_NEO_HOOKEAN && !(e && e[0] == '1')) P.corder = nullptr;
+  }
   const int64_t nc = P.M.ncells;
   const int64_t rec_bytes = align256((int64_t)sizeof(double) * R::SIZE * nc);
   if (W.mode == GatherStage::SIZE) {
