@@ -316,7 +316,7 @@ def main():
         torch.cuda.synchronize()
         t2 = time.time()
         for part in range(len(A.parts)):
-            fem.gather_plan(V, A, part)  # gather plan (chunks, slot map, LDS bank order)
+            fem.gather_plan(V, A, part, a.kind)  # gather plan of the form (chunks, slot map, LDS order)
         torch.cuda.synchronize()
         t_pattern, t_plan = t2 - t1, time.time() - t2
         ncells_local = m.num_cells

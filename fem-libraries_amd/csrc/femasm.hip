@@ -858,6 +858,19 @@ __global__ void k_bc_diag(BsrView A, int64_t nnodes, const int8_t* __restrict__ 
 #define FA_GATHER_LDS 28672
 #endif
 static constexpr int kGatherLdsValues = FA_GATHER_LDS;  // accumulator bytes per workgroup (4 WG / CU)
+// neo-Hookean gather (2 workgroups / CU, VGPR-bound): a larger accumulator, and chunks capped at
+// 256 / NSPLIT adjacency entries so one chunk's items fill the workgroup's 256 lanes once
+// (fa_plan_gather_form); with the default plan ~96 entries -> 192 items left a wave idle
+#ifndef FA_GATHER_LDS_NEO
+#define FA_GATHER_LDS_NEO 46080
+#endif
+static constexpr int kGatherLdsNeo = FA_GATHER_LDS_NEO;
+static constexpr int kGatherNeoEntries = 128;
+// blocks of the accumulator of a gather kernel (the plan's chunks must fit it)
+__host__ __device__ constexpr int gather_maxb(bool neo, int bs2) {
+  return (neo ? kGatherLdsNeo : kGatherLdsValues) / (8 * bs2) < 1023 ? (neo ? kGatherLdsNeo : kGatherLdsValues) / (8 * bs2)
+                                                                      : 1023;
+}
 static constexpr int kGatherMaxAdj = 512;       // adjacency entries per chunk
 static constexpr int kGatherMaxRows = 128;      // rows per chunk
 
@@ -905,6 +918,7 @@ struct GatherArgs {
   const int64_t* chunk_b;  // [nchunks + 1] indptr[row_start[c]] (k_chunk_desc)
   const int64_t* chunk_a;  // [nchunks + 1] adj_ptr[row_start[c]]
   int64_t nchunks;
+  int32_t plan_maxb;        // largest block count of a chunk of the plan (checked against the kernel's)
   unsigned long long* ctr;  // [8] per-XCD chunk counters (dynamic persistent grid), or NULL
   const uint16_t* slots;  // optional [adjacency entry][NN] position of the block within its row
   int slot_order;         // 0, or the NSPLIT whose item order fa_plan_order baked into `slots`
@@ -1377,7 +1391,7 @@ __global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES
 void k_gather(GatherArgs P) {
   using R = Rec<GD, NV, NQ, MAT>;
   constexpr int BS2 = GD * GD;
-  constexpr int MAXB = kGatherLdsValues / (8 * BS2);
+  constexpr int MAXB = gather_maxb(MAT == FA_NEO_HOOKEAN, BS2);
   // ordered slots pack (b << 10) | chunk-relative position: positions must stay below 1024
   static_assert(MAXB < 1024, "FA_GATHER_LDS too large for the packed ordered-slot map");
   constexpr bool SIMP = R::SIMP;
@@ -3108,8 +3122,9 @@ __global__ void k_check_affine(MeshView M, int* nonaffine) {
   }
 }
 
-extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int64_t* row_start,
-                              fa_plan* plan, void* stream) {
+// chunk rows so each chunk's blocks fit `maxb` accumulator blocks and its adjacency `maxadj`
+static int plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int64_t* row_start,
+                       fa_plan* plan, void* stream, int64_t maxb, int maxadj) {
   int rc = check_mesh(mesh);
   if (rc) return rc;
   if (!adj || !A || !row_start || !plan) return fail(FA_E_ARG, "null argument");
@@ -3118,8 +3133,6 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
   if (re0 <= rb0) { rb0 = 0; re0 = mesh->nnodes; }
   if (rb0 < 0 || re0 > mesh->nnodes) return fail(FA_E_ARG, "row window out of range");
   const int64_t n = re0;
-  const int bs2 = mesh->gdim * mesh->gdim;
-  const int64_t maxb = kGatherLdsValues / (8 * bs2);
   std::vector<int64_t> ip(n + 1), ap(n + 1);
   HIP_TRY(hipMemcpyAsync(ip.data(), A->indptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(ap.data(), adj->ptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, s));
@@ -3134,8 +3147,9 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
     if (rb > maxb || ra > kGatherMaxAdj)
       return fail(FA_E_CAPACITY, "row %lld has %lld blocks / %lld cells (gather caps %lld / %d): use FA_SCATTER",
                   (long long)r, (long long)rb, (long long)ra, (long long)maxb, kGatherMaxAdj);
+    // maxadj is a target: a row with more entries gets a chunk of its own
     int64_t cb = ip[r + 1] - ip[start], ca = ap[r + 1] - ap[start];
-    if (cb > maxb || ca > kGatherMaxAdj || r + 1 - start > kGatherMaxRows) {
+    if (r > start && (cb > maxb || ca > maxadj || r + 1 - start > kGatherMaxRows)) {
       rs.push_back(r);
       mb = std::max<int32_t>(mb, (int32_t)(ip[r] - ip[start]));
       ma = std::max<int32_t>(ma, (int32_t)(ap[r] - ap[start]));
@@ -3173,6 +3187,21 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
   plan->eadj = nullptr;
   plan->corder = nullptr;
   return FA_OK;
+}
+
+extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int64_t* row_start,
+                              fa_plan* plan, void* stream) {
+  if (!mesh) return fail(FA_E_ARG, "null mesh");
+  return plan_gather(mesh, adj, A, row_start, plan, stream, gather_maxb(false, mesh->gdim * mesh->gdim),
+                     kGatherMaxAdj);
+}
+
+extern "C" int fa_plan_gather_form(const fa_mesh* mesh, int32_t kind, const fa_adjacency* adj, const fa_bsr* A,
+                                   int64_t* row_start, fa_plan* plan, void* stream) {
+  if (!mesh) return fail(FA_E_ARG, "null mesh");
+  if (kind != FA_NEO_HOOKEAN) return fa_plan_gather(mesh, adj, A, row_start, plan, stream);
+  return plan_gather(mesh, adj, A, row_start, plan, stream, gather_maxb(true, mesh->gdim * mesh->gdim),
+                     kGatherNeoEntries);
 }
 
 // ------------------------------------------------------------------------------- chunk locality order
@@ -3419,6 +3448,9 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     P.eadj = nullptr;
   }
   static_assert(NN * GD <= 32 || MAT == MAT_AFFT, "bc mask holds 32 dofs");
+  if (P.plan_maxb > gather_maxb(MAT == FA_NEO_HOOKEAN, GD * GD))
+    return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, this form's kernel %d: plan with fa_plan_gather_form",
+                P.plan_maxb, gather_maxb(MAT == FA_NEO_HOOKEAN, GD * GD));
   // locality order: pays where the records are large (neo-Hookean tangents, 1.5 KB per cell:
   // 342 -> 328 ms on config E-neo); the 80-B linear records stay in L2 in row order (E: 50.0 vs
   // 51.5 ms in Morton order). FEMASM_CHUNK_ORDER_ALL=1 applies it to every kernel.
@@ -3683,7 +3715,7 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
       return fail(FA_E_ARG, "FA_GATHER needs the adjacency and a plan (fa_plan_gather)");
     GatherArgs P;
     P.M = M; P.F = F; P.A = Av;
-    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks; P.corder = plan->corder;
+    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks; P.corder = plan->corder; P.plan_maxb = plan->max_blocks;
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;
@@ -3761,7 +3793,7 @@ static int gather_stage(const fa_mesh* mesh, const fa_form* form, const fa_adjac
     if (!adj || !adj->ptr || !adj->idx || !plan || !plan->row_start)
       return fail(FA_E_ARG, "fa_gather_rows needs the adjacency and a plan (fa_plan_gather)");
     P.A = BsrView{A->indptr, A->indices, A->data, wb, we};
-    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks; P.corder = plan->corder;
+    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks; P.corder = plan->corder; P.plan_maxb = plan->max_blocks;
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;

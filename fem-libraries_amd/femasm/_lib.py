@@ -97,6 +97,7 @@ SIGNATURES = {
     "fa_sparsity_count": (ctypes.c_int, [P, P, P, P, P]),
     "fa_sparsity_fill": (ctypes.c_int, [P, P, P, P, P]),
     "fa_plan_gather": (ctypes.c_int, [P, P, P, P, P, P]),
+    "fa_plan_gather_form": (ctypes.c_int, [P, I32, P, P, P, P, P]),
     "fa_plan_slots": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_plan_order": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_plan_locality": (ctypes.c_int, [P, P, P, P, P]),

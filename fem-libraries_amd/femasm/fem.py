@@ -508,10 +508,12 @@ def _plan_locality(V, fm, adj, plan, sh):
     return corder if plan.corder else None
 
 
-def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0):
-    """Row-chunk plan of the gather kernel for one row part of A's pattern (cached on V)."""
+def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.FA_LINEAR_ELASTICITY):
+    """Row-chunk plan of the gather kernel of a form kind for one row part of A's pattern (cached
+    on V). Neo-Hookean forms get their own chunking (fa_plan_gather_form); the other kinds share one."""
     plans = V.__dict__.setdefault("_plans", {})
-    key = (A.indptr.data_ptr(), A.parts[part][0], A.parts[part][1])
+    neo = kind == _lib.FA_NEO_HOOKEAN
+    key = (A.indptr.data_ptr(), A.parts[part][0], A.parts[part][1]) + (("neo",) if neo else ())
     if key not in plans:
         L = _lib.load()
         fm = V._fa_mesh()
@@ -520,8 +522,8 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0):
         rs = torch.empty(A.parts[part][1] - A.parts[part][0] + 1, dtype=torch.int64, device=V.mesh.device)
         plan = _lib.fa_plan()
         sh = _lib.stream_handle(V.mesh.device)
-        _lib.check(L.fa_plan_gather(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), rs.data_ptr(),
-                                    ctypes.byref(plan), sh), "fa_plan_gather")
+        _lib.check(L.fa_plan_gather_form(ctypes.byref(fm), int(kind), ctypes.byref(adj), ctypes.byref(fb),
+                                         rs.data_ptr(), ctypes.byref(plan), sh), "fa_plan_gather_form")
         slots = eadj = None
         mode = os.environ.get("FEMASM_SLOTS", "auto")
         # Per (adjacency entry, column node) block position in its row: no LDS search in the
@@ -532,7 +534,8 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0):
             slots = torch.empty(V.mesh.num_cells * V.nn * V.nn, dtype=torch.int16, device=V.mesh.device)
             _lib.check(L.fa_plan_slots(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), slots.data_ptr(),
                                        ctypes.byref(plan), sh), "fa_plan_slots")
-            eadj = _plan_order(V, fm, adj, fb, plan, sh)
+            if not neo:  # the ordered map serves the affine-simplex linear kernels only
+                eadj = _plan_order(V, fm, adj, fb, plan, sh)
         corder = _plan_locality(V, fm, adj, plan, sh)
         plans[key] = (plan, rs, A.indptr, slots, eadj, corder)
     return plans[key][0]
@@ -557,7 +560,7 @@ def assemble_matrix(a, bcs=None, diagonal: float = 1.0, A: MatrixCSR | None = No
         fb = _fa_bsr(A, part)
         if method == "gather":
             adj = V._fa_adjacency()
-            plan = gather_plan(V, A, part)
+            plan = gather_plan(V, A, part, a.kind)
             rc = L.fa_assemble_matrix(ctypes.byref(fm), ctypes.byref(ff), ctypes.byref(adj), ctypes.byref(plan),
                                       _lib.ptr(marker), float(diagonal), ctypes.byref(fb), _lib.FA_GATHER, sh)
         elif method == "scatter":
@@ -605,8 +608,9 @@ class SplitGather:
             rs = torch.empty(r1 - r0 + 1, dtype=torch.int64, device=dev)
             plan = _lib.fa_plan()
             if r1 > r0:
-                _lib.check(L.fa_plan_gather(ctypes.byref(self.fm), ctypes.byref(self.adj), ctypes.byref(fb),
-                                            rs.data_ptr(), ctypes.byref(plan), self.sh), "fa_plan_gather")
+                _lib.check(L.fa_plan_gather_form(ctypes.byref(self.fm), int(a.kind), ctypes.byref(self.adj),
+                                                 ctypes.byref(fb), rs.data_ptr(), ctypes.byref(plan), self.sh),
+                           "fa_plan_gather_form")
             self.subs.append(fb)
             self.plans.append(plan)
             self._keep.append(rs)
@@ -622,6 +626,8 @@ class SplitGather:
             for i in live:
                 self.plans[i].slots = self.slots.data_ptr()
                 self.plans[i].slot_order = 0
+                if a.kind == _lib.FA_NEO_HOOKEAN:
+                    continue  # the neo-Hookean kernel reads the plain slot map
                 e = _plan_order(V, self.fm, self.adj, self.subs[i], self.plans[i], self.sh, self.eadj)
                 self.eadj = e if e is not None else self.eadj
 

@@ -149,6 +149,13 @@ int fa_sparsity_fill(const fa_mesh* mesh, const fa_adjacency* adj, const int64_t
 int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int64_t* row_start, fa_plan* plan,
                    void* stream);
 
+/* fa_plan_gather for the kernel of a form kind: FA_NEO_HOOKEAN chunks fill a larger accumulator
+ * and aim at 128 adjacency entries (one round of the workgroup's 256 item lanes); other kinds are
+ * fa_plan_gather. fa_assemble_matrix refuses a plan whose chunks exceed the form kernel's
+ * accumulator (FA_E_ARG). */
+int fa_plan_gather_form(const fa_mesh* mesh, int32_t kind, const fa_adjacency* adj, const fa_bsr* A,
+                        int64_t* row_start, fa_plan* plan, void* stream);
+
 /* Optional slot map for the gather plan (removes the per-block column search): slots is a
  * caller-owned device buffer of ncells*nn*nn uint16; on success plan->slots points to it.
  * Fails with FA_E_CAPACITY if a row holds more than 65535 blocks. */
