@@ -521,6 +521,51 @@ __device__ void neo_stress_ad(const double (&F)[GD * GD], double lam, double mu,
   }
 }
 
+// The same potential in its invariants, W(I1, J) = mu/2 (I1 - 3) - mu ln J + lam/2 (ln J)^2 with
+// I1 = F:F (+ 1 in 2-D plane strain), psi(F) = W(I1(F), J(F)).
+template <class T>
+__device__ __forceinline__ T neo_energy(const T& I1, const T& J, double lam, double mu) {
+  const T lnJ = ad_log(J);
+  return (0.5 * mu) * (I1 + (-3.0)) - mu * lnJ + (0.5 * lam) * (lnJ * lnJ);
+}
+
+// Tangent coefficients by forward-over-forward AD of W(I1, J) (three hyper-dual passes over the two
+// invariants, seeds unrolled): with C = cof F = dJ/dF and dI1/dF = 2F,
+//   d2psi/dF_iJ dF_kL = 4 W_11 F_iJ F_kL + 2 W_1J (F_iJ C_kL + C_iJ F_kL) + W_JJ C_iJ C_kL
+//                       + 2 W_1 d_ik d_JL + W_J (C_iJ C_kL - C_iL C_kJ) / J,
+// so a block of the element matrix needs F, C and co = {4 W_11, 2 W_1J, W_JJ + W_J / J, W_J / J, 2 W_1}.
+__device__ __forceinline__ void neo_energy_coeffs(double I1, double J, double lam, double mu, double (&co)[5]) {
+  using DD = Dual<Dual<double>>;
+  double W[2][2], G[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = a; b < 2; ++b) {
+      const DD x1{{I1, a == 0 ? 1.0 : 0.0}, {b == 0 ? 1.0 : 0.0, 0.0}};
+      const DD xJ{{J, a == 1 ? 1.0 : 0.0}, {b == 1 ? 1.0 : 0.0, 0.0}};
+      const DD r = neo_energy(x1, xJ, lam, mu);
+      W[a][b] = W[b][a] = r.d.d;
+      G[a] = r.v.d;
+    }
+  co[0] = 4.0 * W[0][0];
+  co[1] = 2.0 * W[0][1];
+  co[2] = W[1][1] + G[1] / J;
+  co[3] = G[1] / J;
+  co[4] = 2.0 * G[0];
+}
+
+// cofactor matrix C = dJ/dF of a row-major F (F[i * GD + J])
+template <int GD>
+__device__ __forceinline__ void cofactor(const double (&F)[GD * GD], double (&C)[GD][GD]) {
+  if constexpr (GD == 2) {
+    C[0][0] = F[3]; C[0][1] = -F[2]; C[1][0] = -F[1]; C[1][1] = F[0];
+  } else {
+    C[0][0] = F[4] * F[8] - F[5] * F[7]; C[0][1] = F[5] * F[6] - F[3] * F[8]; C[0][2] = F[3] * F[7] - F[4] * F[6];
+    C[1][0] = F[2] * F[7] - F[1] * F[8]; C[1][1] = F[0] * F[8] - F[2] * F[6]; C[1][2] = F[1] * F[6] - F[0] * F[7];
+    C[2][0] = F[1] * F[5] - F[2] * F[4]; C[2][1] = F[2] * F[3] - F[0] * F[5]; C[2][2] = F[0] * F[4] - F[1] * F[3];
+  }
+}
+
 // F at a quadrature point from the cell's nodal displacements and physical gradients.
 template <int GD>
 __device__ __forceinline__ void deformation_gradient(const double* __restrict__ u, const int32_t* cn, int nn,
@@ -865,7 +910,13 @@ static constexpr int kGatherLdsValues = FA_GATHER_LDS;  // accumulator bytes per
 #define FA_GATHER_LDS_NEO 46080
 #endif
 static constexpr int kGatherLdsNeo = FA_GATHER_LDS_NEO;
-static constexpr int kGatherNeoEntries = 128;
+#ifndef FA_NEO_NSPLIT
+#define FA_NEO_NSPLIT 2  // column items of 5 columns; see dispatch_gather
+#endif
+static constexpr int kGatherNeoEntries = 256 / FA_NEO_NSPLIT;
+#ifndef FA_GATHER_ENTRY_CAP
+#define FA_GATHER_ENTRY_CAP 512  // adjacency entries per chunk of the default plan (512 = the LDS arrays' cap)
+#endif
 // blocks of the accumulator of a gather kernel (the plan's chunks must fit it)
 __host__ __device__ constexpr int gather_maxb(bool neo, int bs2) {
   return (neo ? kGatherLdsNeo : kGatherLdsValues) / (8 * bs2) < 1023 ? (neo ? kGatherLdsNeo : kGatherLdsValues) / (8 * bs2)
@@ -888,6 +939,10 @@ constexpr int MAT_LINU = 10;
 // gather for Q1-Q3 hexahedra of a structured mesh, with no element-matrix store
 constexpr int MAT_AFFT = 11;
 
+#ifndef FA_NEO_INV
+#define FA_NEO_INV 1  // neo-Hookean records: AD of the strain energy in its invariants (F + 5 scalars per
+                      // point) instead of the 45-entry AD tangent per point
+#endif
 template <int GD, int NV, int NQ, int MAT>
 struct Rec {
   static constexpr bool SIMP = (NV == GD + 1) || MAT == MAT_AFFT;  // affine: one Jacobian per cell
@@ -895,10 +950,15 @@ struct Rec {
   static constexpr int NTRI = N * (N + 1) / 2;  // stored upper triangle of the tangent
   // LIN simplex: Ji[GD*GD], wdet, lam, mu | LINU (simplex): s Ji[GD*GD], sign(mu wdet) | LIN tensor: NQ x (Ji[GD*GD], wdet), lam, mu |
   // DAMAGE (P1 tri): g[3][2], w, H[3][3] | NEO (simplex): Ji[GD*GD], wdet, NQ x A_q upper triangle
+  // NEO per quadrature point (FA_NEO_INV): F[GD*GD] and the strain-energy coefficients s11, s1J,
+  // sCC, sCt, s1 (neo_energy_coeffs) from QOFF, stride QSTR; FA_NEO_INV=0: the 45-entry upper
+  // triangle of dP/dF at N + 1, stride NTRI
+  static constexpr int QOFF = FA_NEO_INV ? ((N + 2) & ~1) : N + 1;
+  static constexpr int QSTR = FA_NEO_INV ? ((N + 6) & ~1) : NTRI;
   static constexpr int RAW = MAT == MAT_BLOCKS ? 2
                              : (MAT == MAT_LINU || MAT == MAT_AFFT) ? GD * GD + 1
                              : MAT == FA_ASYM_DAMAGE ? 16
-                             : MAT == FA_NEO_HOOKEAN ? N + 1 + NQ * NTRI
+                             : MAT == FA_NEO_HOOKEAN ? QOFF + NQ * QSTR
                                                      : (SIMP ? GD * GD + 3 : NQ * (GD * GD + 1) + 2);
   static constexpr int SIZE = (RAW + 1) & ~1;  // even: 16-byte aligned records
 };
@@ -957,12 +1017,31 @@ __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, co
 #pragma unroll
       for (int k = 0; k < GD; ++k) out[i * GD + k] = Ji[i][k];
     out[N] = det;
+    if (R::QOFF > N + 1) out[N + 1] = 0.0;
     double lam, mu;
     cell_lame(F, c, lam, mu);
     const int32_t* cn = M.cells + c * NN;
     for (int q = 0; q < NQ; ++q) {
       double Fq[N];
       deformation_gradient<GD>(F.u, cn, NN, tab + NQ + q * NN * GD, Ji, Fq);
+      if constexpr (FA_NEO_INV) {
+        double I1 = GD == 2 ? 1.0 : 0.0, J;
+#pragma unroll
+        for (int m = 0; m < N; ++m) I1 = fma(Fq[m], Fq[m], I1);
+        if constexpr (GD == 2) J = Fq[0] * Fq[3] - Fq[1] * Fq[2];
+        else J = Fq[0] * (Fq[4] * Fq[8] - Fq[5] * Fq[7]) - Fq[1] * (Fq[3] * Fq[8] - Fq[5] * Fq[6]) +
+                 Fq[2] * (Fq[3] * Fq[7] - Fq[4] * Fq[6]);
+        double co[5];
+        neo_energy_coeffs(I1, J, lam, mu, co);
+        double* o = out + R::QOFF + q * R::QSTR;
+#pragma unroll
+        for (int m = 0; m < N; ++m) o[m] = Fq[m];
+#pragma unroll
+        for (int t = 0; t < 5; ++t) o[N + t] = co[t];
+#pragma unroll
+        for (int t = N + 5; t < R::QSTR; ++t) o[t] = 0.0;
+        continue;
+      }
       using DD = Dual<Dual<double>>;
       // the n(n+1)/2 hyper-dual passes unrolled: with compile-time one-hot seeds the compiler drops
       // the zero derivative terms and evaluates the primal parts (F:F, det F, its log and inverse)
@@ -974,7 +1053,7 @@ __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, co
           DD x[N];
 #pragma unroll
           for (int m = 0; m < N; ++m) x[m] = DD{{Fq[m], m == i ? 1.0 : 0.0}, {m == j ? 1.0 : 0.0, 0.0}};
-          out[N + 1 + q * R::NTRI + tri_index(i, j, N)] = neo_psi<GD, DD>(x, lam, mu).d.d;
+          out[R::QOFF + q * R::QSTR + tri_index(i, j, N)] = neo_psi<GD, DD>(x, lam, mu).d.d;
         }
     }
   } else {
@@ -1373,21 +1452,13 @@ __device__ __forceinline__ int gather_perm(int jj, int na, int st, float inv) {
 #ifndef FA_BARY_WAVES
 #define FA_BARY_WAVES FA_GATHER_WAVES
 #endif
-#ifndef FA_NEOC_WAVES
-#define FA_NEOC_WAVES 3  // component neo-Hookean items keep a row of every column's block live (168 VGPRs)
-#endif
-// neo-Hookean column items: the per-q tangent (45 values) and C (27) are live together
+// neo-Hookean column items (5 columns of K and their gradients live)
 #ifndef FA_NEO_WAVES
 #define FA_NEO_WAVES 2  // 5 columns x (P, K) + a tangent sub-block live: 242 VGPRs, no spills in the item
 #endif
-// neo-Hookean P2-tet items by output component (VAR = 2): FA_NEO_COMPG column groups per
-// component, NSPLIT = gdim * groups (0: column items, NSPLIT = FA_NEO_NSPLIT)
-#ifndef FA_NEO_COMPG
-#define FA_NEO_COMPG 0
-#endif
 template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT, int VAR = 0>
 __global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES
-                                  : (MAT == FA_NEO_HOOKEAN ? (VAR == 2 ? FA_NEOC_WAVES : FA_NEO_WAVES) : FA_GATHER_WAVES))
+                                  : (MAT == FA_NEO_HOOKEAN ? FA_NEO_WAVES : FA_GATHER_WAVES))
 void k_gather(GatherArgs P) {
   using R = Rec<GD, NV, NQ, MAT>;
   constexpr int BS2 = GD * GD;
@@ -1770,93 +1841,6 @@ void k_gather(GatherArgs P) {
         s = s < 0 ? MAXB : s;
         lds_add_block<2>(acc, s, K, (mask >> (aloc * 2)) & 3u, (mask >> (b * 2)) & 3u);
       }
-    } else if constexpr (NEO && VAR == 2) {
-      // Component items (VAR = 2, NSPLIT = gdim * G): item (entry, i, g) computes row i of K_ab for
-      // the g-th group of the cell's columns b: per quadrature point C[k][L] = sum_J ga[J]
-      // A_q[(iJ)(kL)] (9 values from 27 tangent entries) once, then K_ab[i][k] += sum_L C[k][L]
-      // gb[L] for every b of the group -- the contraction is shared by the group's columns instead
-      // of recomputed per column, and a record is read by gdim * G items instead of NN.
-      static_assert(NSPLIT % GD == 0, "component items: NSPLIT = gdim * groups");
-      constexpr int NG = NSPLIT / GD;            // column groups
-      constexpr int NC = (NN + NG - 1) / NG;     // columns per group
-      constexpr int N = R::N;
-      const int ic = part % GD;  // the output component of this item
-      const int cb0 = (part / GD) * NC;  // its first column
-      const double* Aq0 = P.rec + c * R::SIZE + N + 1;
-      const double wdet = r[BS2];
-      int slb[NC];  // slots of the group's columns, loaded before the contraction (independent of it)
-#pragma unroll
-      for (int bb = 0; bb < NC; ++bb) {
-        const int b = min(cb0 + bb, NN - 1);
-        slb[bb] = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_slot(cols, lo, hi, P.M.cells[c * NN + b], niter);
-      }
-      double Kr[NC][GD];
-#pragma unroll
-      for (int bb = 0; bb < NC; ++bb)
-#pragma unroll
-        for (int k = 0; k < GD; ++k) Kr[bb][k] = 0.0;
-#pragma unroll 1
-      for (int q = 0; q < NQ; ++q) {
-        double ga[GD];
-#pragma unroll
-        for (int d = 0; d < GD; ++d) {
-          double sgd = 0.0;
-#pragma unroll
-          for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + aloc) * GD + k] * r[k * GD + d];
-          ga[d] = s_w[q] * wdet * sgd;
-        }
-        const double* Aq = Aq0 + q * R::NTRI;
-        double C[GD][GD];
-#pragma unroll
-        for (int k = 0; k < GD; ++k)
-#pragma unroll
-          for (int L = 0; L < GD; ++L) {
-            double t = 0.0;
-#pragma unroll
-            for (int J = 0; J < GD; ++J) {
-              const int row = ic * GD + J, col = k * GD + L;
-              // symmetric storage, upper triangle: row <= col ? (row, col) : (col, row)
-              const int ti = row <= col ? row * N - row * (row - 1) / 2 + (col - row) : col * N - col * (col - 1) / 2 + (row - col);
-              t = fma(ga[J], Aq[ti], t);
-            }
-            C[k][L] = t;
-          }
-#pragma unroll
-        for (int bb = 0; bb < NC; ++bb) {
-          const int b = min(cb0 + bb, NN - 1);
-          double gb[GD];
-#pragma unroll
-          for (int d = 0; d < GD; ++d) {
-            double sgd = 0.0;
-#pragma unroll
-            for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + b) * GD + k] * r[k * GD + d];
-            gb[d] = sgd;
-          }
-#pragma unroll
-          for (int k = 0; k < GD; ++k) {
-            double t = Kr[bb][k];
-#pragma unroll
-            for (int L = 0; L < GD; ++L) t = fma(C[k][L], gb[L], t);
-            Kr[bb][k] = t;
-          }
-          __builtin_amdgcn_sched_barrier(0);  // one column at a time: bounds the live table reads
-        }
-      }
-      // row dof (aloc, ic) constrained: the whole row of every block is zero; column dof (b, k): entry k
-      const bool rowc = (mask >> (aloc * GD + ic)) & 1u;
-#pragma unroll
-      for (int bb = 0; bb < NC; ++bb) {
-        const int b = cb0 + bb;
-        if (NN % NG != 0 && b >= NN) break;
-        int sb = slb[bb];
-        bad |= sb < 0;
-        sb = sb < 0 ? MAXB : sb;
-#pragma unroll
-        for (int k = 0; k < GD; ++k) {
-          const double v = (rowc || ((mask >> (b * GD + k)) & 1u)) ? 0.0 : Kr[bb][k];
-          atomicAdd(&acc[sb * BS2 + ic * GD + k], v);
-        }
-      }
     } else if constexpr (NEO) {
       // K_ab[i][k] = sum_q sum_{J,L} P[J][L] A_q[(iJ)(kL)] with P = (w_q |J| ga) (x) gb: the outer
       // product first, then each 3x3 sub-block A_ik of the symmetric tangent is read once and serves
@@ -1864,7 +1848,7 @@ void k_gather(GatherArgs P) {
       // where contracting the row gradient first (C[i][k][L], 27 values) held C and all 45 tangent
       // values at once and spilled (133 VGPRs at 4 waves / SIMD).
       constexpr int N = R::N;
-      const double* Aq0 = P.rec + c * R::SIZE + N + 1;
+      const double* Aq0 = P.rec + c * R::SIZE + R::QOFF;
       const double wdet = r[BS2];
       double K[NBG][GD][GD];
 #pragma unroll
@@ -1883,7 +1867,6 @@ void k_gather(GatherArgs P) {
           for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + aloc) * GD + k] * r[k * GD + d];
           ga[d] = s_w[q] * wdet * sgd;
         }
-        const double* Aq = Aq0 + q * R::NTRI;
         double gb[NBG][GD];  // column gradients of the item
 #pragma unroll
         for (int bb = 0; bb < NBG; ++bb) {
@@ -1896,6 +1879,69 @@ void k_gather(GatherArgs P) {
             gb[bb][d] = sgd;
           }
         }
+        if constexpr (FA_NEO_INV) {
+          // invariant form (neo_energy_coeffs): K_ab += co2 Ca Cb^T - co3 Cb Ca^T + co4 (ga.gb) I
+          // [+ co0 Fa Fb^T + co1 (Fa Cb^T + Ca Fb^T)], Fa = F ga, Ca = C ga: 14 values per point
+          const double* Qq = P.rec + c * R::SIZE + R::QOFF + q * R::QSTR;
+          double Fq[N], co[5];
+#pragma unroll
+          for (int m = 0; m < N; ++m) Fq[m] = Qq[m];
+#pragma unroll
+          for (int t = 0; t < 5; ++t) co[t] = Qq[N + t];
+          double Cm[GD][GD];
+          cofactor<GD>(Fq, Cm);
+          double u[GD], v[GD], w[GD];
+#pragma unroll
+          for (int i = 0; i < GD; ++i) {
+            double ca = 0.0, fa = 0.0;
+#pragma unroll
+            for (int J = 0; J < GD; ++J) {
+              ca = fma(Cm[i][J], ga[J], ca);
+              fa = fma(Fq[i * GD + J], ga[J], fa);
+            }
+            u[i] = co[2] * ca + co[1] * fa;  // multiplies Cb_k
+            v[i] = co[3] * ca;               // K_ik -= Cb_i v_k
+            w[i] = co[0] * fa + co[1] * ca;  // multiplies Fb_k
+          }
+          // W_11 = W_1J = 0 for this energy: the F terms only where a lane has them (wave-uniform)
+          const bool mixed = __any(co[0] != 0.0 || co[1] != 0.0);
+#pragma unroll
+          for (int bb = 0; bb < NBG; ++bb) {
+            double Cb[GD], dot = 0.0;
+#pragma unroll
+            for (int k = 0; k < GD; ++k) {
+              double t = 0.0;
+#pragma unroll
+              for (int L = 0; L < GD; ++L) t = fma(Cm[k][L], gb[bb][L], t);
+              Cb[k] = t;
+              dot = fma(ga[k], gb[bb][k], dot);
+            }
+#pragma unroll
+            for (int i = 0; i < GD; ++i)
+#pragma unroll
+              for (int k = 0; k < GD; ++k) {
+                double t = fma(u[i], Cb[k], K[bb][i][k]);
+                t = fma(-Cb[i], v[k], t);
+                if (i == k) t = fma(co[4], dot, t);
+                K[bb][i][k] = t;
+              }
+            if (mixed) {
+              double Fb[GD];
+#pragma unroll
+              for (int k = 0; k < GD; ++k) {
+                double t = 0.0;
+#pragma unroll
+                for (int L = 0; L < GD; ++L) t = fma(Fq[k * GD + L], gb[bb][L], t);
+                Fb[k] = t;
+              }
+#pragma unroll
+              for (int i = 0; i < GD; ++i)
+#pragma unroll
+                for (int k = 0; k < GD; ++k) K[bb][i][k] = fma(w[i], Fb[k], K[bb][i][k]);
+            }
+          }
+        } else {
+        const double* Aq = Aq0 + q * R::QSTR;
         // per 3x3 sub-block A_ik of the tangent (loaded once per item): the row gradient is
         // contracted first, C[L] = sum_J ga[J] A_ik[J][L] (and C'[L] = sum_J ga[J] A_ik[L][J] for
         // K[k][i]), then C is applied to every column: 81 + 27 NBG FMAs per point, and only ga, the
@@ -1942,6 +1988,7 @@ void k_gather(GatherArgs P) {
               }
             }
           }
+        }
         }
       }
 #pragma unroll
@@ -3193,7 +3240,7 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
                               fa_plan* plan, void* stream) {
   if (!mesh) return fail(FA_E_ARG, "null mesh");
   return plan_gather(mesh, adj, A, row_start, plan, stream, gather_maxb(false, mesh->gdim * mesh->gdim),
-                     kGatherMaxAdj);
+                     std::min(FA_GATHER_ENTRY_CAP, kGatherMaxAdj));
 }
 
 extern "C" int fa_plan_gather_form(const fa_mesh* mesh, int32_t kind, const fa_adjacency* adj, const fa_bsr* A,
@@ -3615,13 +3662,7 @@ static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const
   const int ct = m->cell_type, p = m->degree, nq = T.nq;
   if (kind == FA_ASYM_DAMAGE) return launch_gather<2, 3, 3, 1, 1, FA_ASYM_DAMAGE>(P, bc, s, W);
   if (kind == FA_NEO_HOOKEAN) {
-    if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) {
-#if FA_NEO_COMPG > 0
-      return launch_gather<3, 10, 4, 4, 3 * FA_NEO_COMPG, FA_NEO_HOOKEAN, 2>(P, bc, s, W);
-#else
-      return launch_gather<3, 10, 4, 4, FA_NEO_NSPLIT, FA_NEO_HOOKEAN>(P, bc, s, W);
-#endif
-    }
+    if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, FA_NEO_NSPLIT, FA_NEO_HOOKEAN>(P, bc, s, W);
     if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, FA_NEO_HOOKEAN>(P, bc, s, W);
     if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, FA_NEO_HOOKEAN>(P, bc, s, W);
     if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, FA_NEO_HOOKEAN>(P, bc, s, W);
