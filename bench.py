@@ -134,7 +134,7 @@ def measured_traffic(config: str, n: int, world: int):
     return rec, rec["source"]
 
 
-def compulsory_bytes(V, A, ncells: int, with_bc: bool) -> dict:
+def compulsory_bytes(V, A, ncells: int, with_bc: bool, state: bool = False) -> dict:
     """Algorithmic bytes of one write-once assembly of A's row window: every matrix
     value written once (8 nnz) plus what any assembler must read -- the BSR pattern (4 B per block +
     8 B per row pointer), the dofmap (4 nn per cell), the geometry dofmap (4 nv per cell at degree
@@ -153,6 +153,7 @@ def compulsory_bytes(V, A, ncells: int, with_bc: bool) -> dict:
         "geometry": (4 * nv * ncells if V.degree > 1 else 0) + 8 * gd * int(m.x.shape[0]),
         "coefficients": 8 * ncells,
         "bc_markers": V.num_dofs if with_bc else 0,
+        "state": 8 * V.num_dofs if state else 0,  # the neo-Hookean form's displacement u
     }
     parts["total"] = sum(parts.values())
     return parts
@@ -367,7 +368,7 @@ def main():
     melem_s = ncells_total / (ms_per_step * 1e-3) / 1e6
     # roofline.achieved: the algorithmic (write-once, compulsory) bytes of this rank's assembly over
     # the live event time of one launch on the launch stream
-    comp = compulsory_bytes(V_loc, A_loc, ncells_local, with_bc)
+    comp = compulsory_bytes(V_loc, A_loc, ncells_local, with_bc, state=cfg.get("form") == "neo")
     achieved = comp["total"] / (launch_ms * 1e-3) / 1e9
     # traffic: PMC-measured HBM bytes per launch of this build (profiles/traffic.json, keyed on the
     # femasm.hip hash), with its own fraction of peak; the SURVEY §8(d) element-stream model B_e is
@@ -378,14 +379,19 @@ def main():
     fracs = {"frac": achieved / HBM_PEAK_GBPS}
     f_e = flops_per_cell(cfg)
     tflops = f_e * ncells_local / (launch_ms * 1e-3) / 1e12
-    fracs["flop_frac"] = tflops / FP64_PEAK_TFLOPS
-    compute_bound = cfg.get("form") == "neo"  # AI = F_e / algorithmic bytes is above the FP64 ridge
+    # neo-Hookean: FP64-compute-bound (executed flops / algorithmic bytes ~15 flop/B, above the 9.8
+    # flop/B ridge). achieved = the executed FP64 flops of the launch counted by the PMC
+    # (SQ_INSTS_VALU_FLOPS_FP64, profiles/traffic.json of this build); F_e stays a model
+    compute_bound = cfg.get("form") == "neo"
+    exec_flops = None if trec is None else trec.get("fp64_flops")
+    tflops_exec = None if exec_flops is None else exec_flops / (launch_ms * 1e-3) / 1e12
+    fracs["flop_frac"] = (tflops_exec if tflops_exec is not None else tflops) / FP64_PEAK_TFLOPS
     if traffic_gbps is not None:
         fracs["traffic_frac"] = traffic_gbps / HBM_PEAK_GBPS
     # the fractions reported as measured must be physical; F_e is the quadrature contraction's
     # flop count, a model for kernels that do not run it (the affine reference-tensor gathers)
     for k, v in fracs.items():
-        if k != "flop_frac" or compute_bound:
+        if k != "flop_frac" or tflops_exec is not None:
             assert v <= 1.0, f"roofline {k} = {v:.3f} > 1: a byte count or a time is wrong"
 
     cpu = None
@@ -443,19 +449,23 @@ def main():
                        if world > 1 else "single GPU"},
             # per GPU (rank 0 / slowest rank): achieved = algorithmic bytes of the assembly / launch time
             "roofline": {"bound": "mfma" if compute_bound else "hbm",
-                         "achieved": round(tflops, 3) if compute_bound else round(achieved, 1),
+                         "achieved": round(tflops_exec if tflops_exec is not None else tflops, 3) if compute_bound
+                         else round(achieved, 1),
+                         "achieved_source": ("PMC SQ_INSTS_VALU_FLOPS_FP64 (executed FP64 flops, FP64 VALU; "
+                                             "no MFMA in this kernel)" if tflops_exec is not None else
+                                             "model F_e (no PMC flop record for this build)") if compute_bound
+                         else "algorithmic bytes / launch time",
                          "peak": FP64_PEAK_TFLOPS if compute_bound else HBM_PEAK_GBPS,
                          "unit": "TFLOP/s" if compute_bound else "GB/s",
                          "frac": round(fracs["flop_frac"] if compute_bound else fracs["frac"], 4), "traffic": traffic,
                          "hbm": {"achieved_GBps": round(achieved, 1), "frac": round(fracs["frac"], 4)},
-                         ("fp64" if compute_bound else "model_fp64"): (
-                             {"flops_per_cell": f_e, "achieved_TFLOPs": round(tflops, 3),
-                              "frac": round(fracs["flop_frac"], 4), "peak_TFLOPs": FP64_PEAK_TFLOPS,
-                              "what": "SURVEY §8(d) F_e (B^T D B contraction; AD passes not counted) "
-                                      "x cells / launch time"} if compute_bound else
-                             {"flops_per_cell": f_e, "equivalent_TFLOPs": round(tflops, 3),
-                              "what": "SURVEY §8(d) F_e at this rate: the quadrature contraction's flops, "
-                                      "a model -- the gathers form blocks from reference tensors instead"}),
+                         "model_fp64": {"flops_per_cell": f_e, "equivalent_TFLOPs": round(tflops, 3),
+                                        "what": "SURVEY §8(d) F_e at this rate: the B^T D B quadrature contraction's "
+                                                "flops, a model -- the gathers form blocks from reference tensors "
+                                                "(linear) or from F, cof F and invariant coefficients (neo-Hookean)"},
+                         "fp64_executed": None if exec_flops is None else {
+                             "flops_per_launch": exec_flops, "TFLOPs": round(tflops_exec, 3),
+                             "frac": round(tflops_exec / FP64_PEAK_TFLOPS, 4), "peak_TFLOPs": FP64_PEAK_TFLOPS},
                          "traffic_GBps": None if traffic_gbps is None else round(traffic_gbps, 1),
                          "traffic_frac": None if traffic_gbps is None else round(fracs["traffic_frac"], 4),
                          "traffic_source": tsrc,

@@ -25,6 +25,20 @@ for k, d in acc.items():
         print(f"  {c:24s} {mean:16.1f}{extra}  [{len(per)} dispatches]")
 
 
+def counter_total(name, kernels=("k_gather", "k_cell_records")):
+    """Sum over the launch's kernels of the per-dispatch mean of one counter, or None if not collected."""
+    tot, seen = 0.0, False
+    for k, d in acc.items():
+        if not any(s in k for s in kernels) or name not in d:
+            continue
+        per = defaultdict(float)
+        for did, v in d[name]:
+            per[did] += v
+        tot += sum(per.values()) / len(per)
+        seen = True
+    return tot if seen else None
+
+
 def traffic_record(root, kernels=("k_gather", "k_cell_records")):
     """HBM bytes per assembly launch: sum over the launch's kernels of FETCH_SIZE x 2 + WRITE_SIZE (KB)."""
     tot = 0.0
@@ -54,4 +68,10 @@ if len(sys.argv) > 3:  # pmc_summary.py ROOT KEY OUT_JSON: record traffic for be
     # keyed on the kernel source hash: bench.py refuses a record of another build of femasm.hip
     data[key] = {"bytes": traffic_record(root), "kernel_hash": khash,
                  "source": f"rocprofv3 --pmc passes in {root} (tools/prof_passes.sh)"}
+    fl = counter_total("SQ_INSTS_VALU_FLOPS_FP64")
+    if fl is not None:
+        # SQ_INSTS_VALU_FLOPS_FP64 = 2 FMA + MUL + ADD per wave instruction (measured: it equals that
+        # sum of the SQ_INSTS_VALU_*_F64 counters); x 64 lanes = the FP64 work issued to the VALU
+        data[key]["fp64_flops"] = 64.0 * fl
+        data[key]["fp64_flops_what"] = "64 x SQ_INSTS_VALU_FLOPS_FP64 (lane slots of the issued FP64 VALU instructions)"
     json.dump(data, open(out, "w"), indent=1)
