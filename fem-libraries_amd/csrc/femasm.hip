@@ -1857,6 +1857,107 @@ void k_gather(GatherArgs P) {
         for (int i = 0; i < GD; ++i)
 #pragma unroll
           for (int k = 0; k < GD; ++k) K[bb][i][k] = 0.0;
+      if constexpr (FA_NEO_INV) {
+        // invariant form (neo_energy_coeffs), 14 record values per point, the next point's values
+        // loaded while this one is contracted: per column K_ab += c2 Ca Cb^T - c3 Cb Ca^T +
+        // c4 (ga.gb) I [+ c0 Fa Fb^T + c1 (Fa Cb^T + Ca Fb^T)], Ca = cof(F) ga, Fa = F ga
+        const double* Q0 = P.rec + c * R::SIZE + R::QOFF;
+        constexpr int NL = N + 5;
+        double Qn[NL];
+#pragma unroll
+        for (int t = 0; t < NL; ++t) Qn[t] = Q0[t];
+#pragma unroll 1
+        for (int q = 0; q < NQ; ++q) {
+          double Qc[NL];
+#pragma unroll
+          for (int t = 0; t < NL; ++t) Qc[t] = Qn[t];
+          {
+            const double* Qx = Q0 + min(q + 1, NQ - 1) * R::QSTR;  // next point (the last one re-reads)
+#pragma unroll
+            for (int t = 0; t < NL; ++t) Qn[t] = Qx[t];
+          }
+          double ga[GD];
+#pragma unroll
+          for (int d = 0; d < GD; ++d) {
+            double sgd = 0.0;
+#pragma unroll
+            for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + aloc) * GD + k] * r[k * GD + d];
+            ga[d] = s_w[q] * wdet * sgd;
+          }
+          double Cm[GD][GD];
+          {
+            double Fq[N];
+#pragma unroll
+            for (int m = 0; m < N; ++m) Fq[m] = Qc[m];
+            cofactor<GD>(Fq, Cm);
+          }
+          const double c0 = Qc[N], c1 = Qc[N + 1], c2 = Qc[N + 2], c3 = Qc[N + 3], c4 = Qc[N + 4];
+          double u[GD], v[GD];
+#pragma unroll
+          for (int i = 0; i < GD; ++i) {
+            double ca = 0.0;
+#pragma unroll
+            for (int J = 0; J < GD; ++J) ca = fma(Cm[i][J], ga[J], ca);
+            u[i] = c2 * ca;
+            v[i] = c3 * ca;
+          }
+          // W_11 = W_1J = 0 for this energy: the F terms only where a lane has them (wave-uniform)
+          const bool mixed = __any(c0 != 0.0 || c1 != 0.0);
+          double w[GD];
+          if (mixed) {
+#pragma unroll
+            for (int i = 0; i < GD; ++i) {
+              double ca = 0.0, fa = 0.0;
+#pragma unroll
+              for (int J = 0; J < GD; ++J) {
+                ca = fma(Cm[i][J], ga[J], ca);
+                fa = fma(Qc[i * GD + J], ga[J], fa);
+              }
+              u[i] = fma(c1, fa, u[i]);
+              w[i] = c0 * fa + c1 * ca;
+            }
+          }
+#pragma unroll
+          for (int bb = 0; bb < NBG; ++bb) {
+            const int b = min(part * NBG + bb, NN - 1);  // past-the-end columns: computed, never added
+            double gb[GD], Cb[GD], dot = 0.0;
+#pragma unroll
+            for (int d = 0; d < GD; ++d) {
+              double sgd = 0.0;
+#pragma unroll
+              for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + b) * GD + k] * r[k * GD + d];
+              gb[d] = sgd;
+              dot = fma(ga[d], sgd, dot);
+            }
+#pragma unroll
+            for (int k = 0; k < GD; ++k) {
+              double t = 0.0;
+#pragma unroll
+              for (int L = 0; L < GD; ++L) t = fma(Cm[k][L], gb[L], t);
+              Cb[k] = t;
+            }
+#pragma unroll
+            for (int i = 0; i < GD; ++i)
+#pragma unroll
+              for (int k = 0; k < GD; ++k) {
+                double t = fma(u[i], Cb[k], K[bb][i][k]);
+                t = fma(-Cb[i], v[k], t);
+                if (i == k) t = fma(c4, dot, t);
+                K[bb][i][k] = t;
+              }
+            if (mixed) {
+#pragma unroll
+              for (int k = 0; k < GD; ++k) {
+                double fb = 0.0;
+#pragma unroll
+                for (int L = 0; L < GD; ++L) fb = fma(Qc[k * GD + L], gb[L], fb);
+#pragma unroll
+                for (int i = 0; i < GD; ++i) K[bb][i][k] = fma(w[i], fb, K[bb][i][k]);
+              }
+            }
+          }
+        }
+      } else {
 #pragma unroll 1
       for (int q = 0; q < NQ; ++q) {
         double ga[GD];
@@ -1879,68 +1980,6 @@ void k_gather(GatherArgs P) {
             gb[bb][d] = sgd;
           }
         }
-        if constexpr (FA_NEO_INV) {
-          // invariant form (neo_energy_coeffs): K_ab += co2 Ca Cb^T - co3 Cb Ca^T + co4 (ga.gb) I
-          // [+ co0 Fa Fb^T + co1 (Fa Cb^T + Ca Fb^T)], Fa = F ga, Ca = C ga: 14 values per point
-          const double* Qq = P.rec + c * R::SIZE + R::QOFF + q * R::QSTR;
-          double Fq[N], co[5];
-#pragma unroll
-          for (int m = 0; m < N; ++m) Fq[m] = Qq[m];
-#pragma unroll
-          for (int t = 0; t < 5; ++t) co[t] = Qq[N + t];
-          double Cm[GD][GD];
-          cofactor<GD>(Fq, Cm);
-          double u[GD], v[GD], w[GD];
-#pragma unroll
-          for (int i = 0; i < GD; ++i) {
-            double ca = 0.0, fa = 0.0;
-#pragma unroll
-            for (int J = 0; J < GD; ++J) {
-              ca = fma(Cm[i][J], ga[J], ca);
-              fa = fma(Fq[i * GD + J], ga[J], fa);
-            }
-            u[i] = co[2] * ca + co[1] * fa;  // multiplies Cb_k
-            v[i] = co[3] * ca;               // K_ik -= Cb_i v_k
-            w[i] = co[0] * fa + co[1] * ca;  // multiplies Fb_k
-          }
-          // W_11 = W_1J = 0 for this energy: the F terms only where a lane has them (wave-uniform)
-          const bool mixed = __any(co[0] != 0.0 || co[1] != 0.0);
-#pragma unroll
-          for (int bb = 0; bb < NBG; ++bb) {
-            double Cb[GD], dot = 0.0;
-#pragma unroll
-            for (int k = 0; k < GD; ++k) {
-              double t = 0.0;
-#pragma unroll
-              for (int L = 0; L < GD; ++L) t = fma(Cm[k][L], gb[bb][L], t);
-              Cb[k] = t;
-              dot = fma(ga[k], gb[bb][k], dot);
-            }
-#pragma unroll
-            for (int i = 0; i < GD; ++i)
-#pragma unroll
-              for (int k = 0; k < GD; ++k) {
-                double t = fma(u[i], Cb[k], K[bb][i][k]);
-                t = fma(-Cb[i], v[k], t);
-                if (i == k) t = fma(co[4], dot, t);
-                K[bb][i][k] = t;
-              }
-            if (mixed) {
-              double Fb[GD];
-#pragma unroll
-              for (int k = 0; k < GD; ++k) {
-                double t = 0.0;
-#pragma unroll
-                for (int L = 0; L < GD; ++L) t = fma(Fq[k * GD + L], gb[bb][L], t);
-                Fb[k] = t;
-              }
-#pragma unroll
-              for (int i = 0; i < GD; ++i)
-#pragma unroll
-                for (int k = 0; k < GD; ++k) K[bb][i][k] = fma(w[i], Fb[k], K[bb][i][k]);
-            }
-          }
-        } else {
         const double* Aq = Aq0 + q * R::QSTR;
         // per 3x3 sub-block A_ik of the tangent (loaded once per item): the row gradient is
         // contracted first, C[L] = sum_J ga[J] A_ik[J][L] (and C'[L] = sum_J ga[J] A_ik[L][J] for
@@ -1989,7 +2028,7 @@ void k_gather(GatherArgs P) {
             }
           }
         }
-        }
+      }
       }
 #pragma unroll
       for (int bb = 0; bb < NBG; ++bb) {
