@@ -64,6 +64,10 @@ CONFIGS = {
     "C": dict(cell="tetrahedron", degree=1, n=119, qdeg=None, label="3-D P1 tet, 119^3x6"),
     "D": dict(cell="hexahedron", degree=3, n=58, qdeg=None, label="3-D Q3 hex, 58^3 (192x192 local)"),
     "Dq2": dict(cell="hexahedron", degree=2, n=58, qdeg=None, label="3-D Q2 hex, 58^3 (81x81 local)"),
+    # config D with interior vertices moved (non-affine trilinear cells): the MFMA element kernel +
+    # block-store gather instead of the affine tensor gather
+    "Dmfma": dict(cell="hexahedron", degree=3, n=58, qdeg=None, perturb=0.2,
+                  label="3-D Q3 hex, 58^3, interior vertices moved 0.2 h (non-affine: MFMA element path)"),
     "E": dict(cell="tetrahedron", degree=2, n=203, qdeg=None, label="3-D P2 tet, 203^3x6 (config E mesh)"),
     "Eneo": dict(cell="tetrahedron", degree=2, n=203, qdeg=2, form="neo",
                  label="3-D P2 tet neo-Hookean (AD tangent), 203^3x6, u = 1e-3 sin(pi x)"),
@@ -82,6 +86,16 @@ def bytes_per_cell(cfg):
     return 4 * nn + geom + 8 * gd * nv + 8 + 16 * nd * nd
 
 
+def perturb_vertices(m, amp):
+    """Move interior vertices by amp * sin(2 pi x) sin(pi y) sin(pi z) (per component, phase-shifted):
+    boundary planes stay put (the bcs locate x = 0 and x = 1), trilinear cells become non-affine."""
+    x = m.x
+    s = torch.sin(torch.pi * x).prod(dim=1, keepdim=True)
+    shift = torch.stack([torch.sin(2 * torch.pi * x[:, 0]), torch.cos(2 * torch.pi * x[:, 1]),
+                         torch.sin(2 * torch.pi * x[:, 2] + 0.5)], dim=1)
+    x += amp * s * shift
+
+
 def build_problem(n, dev, z_range=None, cfg=None):
     from femasm import fem, mesh
 
@@ -93,6 +107,8 @@ def build_problem(n, dev, z_range=None, cfg=None):
         m = mesh.create_rectangle((1.0, 1.0), (n, n), ct, device=dev)
     else:
         m = mesh.create_box((1.0, 1.0, 1.0), (n, n, n), ct, device=dev, z_range=z_range)
+    if cfg.get("perturb"):
+        perturb_vertices(m, cfg["perturb"] / n)
     gd = m.gdim
     V = fem.functionspace(m, ("Lagrange", cfg["degree"], (gd,)))
     per_layer = n * n * (6 if ct == mesh.CellType.tetrahedron else 1)

@@ -3,8 +3,9 @@
   A  71 x 71 x 2 P1 triangles (reference J at d = 0, quadrature degree 1, reference bcs): the whole
      matrix against the committed fixture tests/golden/config_a_p1_elasticity.npz (oracle output,
      tests/golden/make_golden.py) -- identical pattern, every row within 1e-12.
-  B  1000 x 1000 Q2 quadrilaterals, C 119^3 x 6 P1 tetrahedra, D 58^3 Q3 hexahedra (the MFMA path),
-  D' 58^3 Q2 hexahedra, E 203^3 x 6 P2 tetrahedra with the neo-Hookean AD tangent: sampled rows of
+  B  1000 x 1000 Q2 quadrilaterals, C 119^3 x 6 P1 tetrahedra, D 58^3 Q3 hexahedra (affine tensor
+  gather) and the same with interior vertices moved (non-affine: the MFMA element path), D' 58^3 Q2
+  hexahedra, E 203^3 x 6 P2 tetrahedra with the neo-Hookean AD tangent: sampled rows of
      the GPU matrix against the oracle assembling exactly the cells adjacent to those rows.
   (Config E with the linear form at full size: tests/test_gpu_fullsize.py.)
 
@@ -38,7 +39,7 @@ def _free_memory():
         torch.cuda.empty_cache()
 
 
-def _problem(ct, degree, n, dev, form="linear", qdeg=None):
+def _problem(ct, degree, n, dev, form="linear", qdeg=None, perturb=0.0):
     from femasm import fem, mesh
     from femasm.materials import e_range
 
@@ -47,6 +48,12 @@ def _problem(ct, degree, n, dev, form="linear", qdeg=None):
         m = mesh.create_unit_square(n, n, cell_type=ct, device=dev)
     else:
         m = mesh.create_unit_cube(n, n, n, cell_type=ct, device=dev)
+    if perturb:  # interior vertices moved (as bench.py --config Dmfma): non-affine trilinear cells
+        x = m.x
+        s = torch.sin(torch.pi * x).prod(dim=1, keepdim=True)
+        shift = torch.stack([torch.sin(2 * torch.pi * x[:, 0]), torch.cos(2 * torch.pi * x[:, 1]),
+                             torch.sin(2 * torch.pi * x[:, 2] + 0.5)], dim=1)
+        x += perturb / n * s * shift
     gd = m.gdim
     V = fem.functionspace(m, ("Lagrange", degree, (gd,)))
     E = torch.tensor(e_range(), dtype=torch.float64, device=dev)[torch.arange(m.num_cells, device=dev) % 200]
@@ -80,23 +87,28 @@ def test_config_a_against_golden_fixture(dev):
 
 
 CONFIGS = [
-    # id, cell, degree, n, rows sampled
-    ("B", "quadrilateral", 2, 1000, 1500),
-    ("C", "tetrahedron", 1, 119, 1500),
-    ("Dq2", "hexahedron", 2, 58, 400),
-    ("D", "hexahedron", 3, 58, 150),
+    # id, cell, degree, n, rows sampled, vertex perturbation (0: affine cells)
+    ("B", "quadrilateral", 2, 1000, 1500, 0.0),
+    ("C", "tetrahedron", 1, 119, 1500, 0.0),
+    ("Dq2", "hexahedron", 2, 58, 400, 0.0),
+    ("D", "hexahedron", 3, 58, 150, 0.0),
+    ("Dmfma", "hexahedron", 3, 58, 100, 0.2),  # non-affine: MFMA element kernel + block gather
 ]
 
 
-@pytest.mark.parametrize("cfg,ct,degree,n,nsample", CONFIGS, ids=[c[0] for c in CONFIGS])
-def test_config_full_size(oracle, dev, cfg, ct, degree, n, nsample):
+@pytest.mark.parametrize("cfg,ct,degree,n,nsample,perturb", CONFIGS, ids=[c[0] for c in CONFIGS])
+def test_config_full_size(oracle, dev, cfg, ct, degree, n, nsample, perturb):
     from femasm import fem
 
-    m, V, a, bcs = _problem(ct, degree, n, dev)
+    m, V, a, bcs = _problem(ct, degree, n, dev, perturb=perturb)
     A = fem.create_matrix(a)
     assert int(A.indptr[-1]) == A.num_blocks
     fem.assemble_matrix(a, bcs=bcs, A=A)
     torch.cuda.synchronize()
+    if ct == "hexahedron":  # the plan's affinity test picks the kernel: affine tensor gather or MFMA
+        from femasm import _lib
+        plan = fem.gather_plan(V, A, 0)
+        assert bool(plan.cell_flags & _lib.FA_PLAN_AFFINE) == (perturb == 0.0)
     marker, _ = fem._combine_bcs(V, bcs)
     # rows on both bc planes and a chunk of consecutive rows are always in the sample
     x = V.tabulate_dof_coordinates()
