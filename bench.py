@@ -271,6 +271,9 @@ def main():
     ap.add_argument("--cpu-reps", type=int, default=7)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true", help="N > 1: exchange after all rows (no overlap)")
+    ap.add_argument("--slab-mode", default="exchange", choices=["exchange", "ghost"],
+                    help="N > 1: RCCL interface exchange (default) or the communication-free redundant "
+                         "ghost layer (SURVEY §8(e) alternative)")
     ap.add_argument("--cpu-cores", type=int, default=0,
                     help="processes of the all-cores CPU baseline (0 = every affinity core, capped by the cgroup "
                          "CPU quota; 1 = single core only)")
@@ -319,7 +322,8 @@ def main():
 
         if args.config not in ("E", "Eneo"):
             raise SystemExit("N > 1 shards config E's mesh (P2 tets; linear elasticity or neo-Hookean) only")
-        prob = parallel.SlabProblem(n, rank, world, dev, form="neo" if args.config == "Eneo" else "linear")
+        prob = parallel.SlabProblem(n, rank, world, dev, form="neo" if args.config == "Eneo" else "linear",
+                                    mode=args.slab_mode)
 
         def step():
             prob.assemble(overlap=not args.no_overlap)
@@ -458,10 +462,13 @@ def main():
                       "what": "setup_s = mesh + function space + bcs + sparsity pattern + gather plan, once "
                               "per mesh (the reference's create_matrix is likewise outside its timed region)"},
             "config": {"workload": workload, "method": args.method,
-                       "parallelism": (f"z-slabs x{world}: interface planes first, 2-rank "
-                                       f"{'RCCL' if backend == 'nccl' else backend} all-reduce of "
-                                       f"their shared blocks per boundary ({exchange_mb} MB max per rank) "
-                                       f"{'after' if args.no_overlap else 'overlapping'} the interior rows")
+                       "parallelism": ((f"z-slabs x{world}: interface planes first, 2-rank "
+                                        f"{'RCCL' if backend == 'nccl' else backend} all-reduce of "
+                                        f"their shared blocks per boundary ({exchange_mb} MB max per rank) "
+                                        f"{'after' if args.no_overlap else 'overlapping'} the interior rows")
+                                       if args.slab_mode == "exchange" else
+                                       f"z-slabs x{world}, no exchange: each rank also assembles the cell layer "
+                                       f"above its slab (redundant ghost layer) so its owned rows are complete")
                        if world > 1 else "single GPU"},
             # per GPU (rank 0 / slowest rank): achieved = algorithmic bytes of the assembly / launch time
             "roofline": {"bound": "mfma" if compute_bound else "hbm",

@@ -64,6 +64,12 @@ class SlabPartition:
         self.upper = None if self.rank == self.world - 1 else (self.row_end - self.plane, self.row_end)
 
     @property
+    def assembly_layers(self) -> tuple[int, int]:
+        """Cell layers whose cells complete every owned row without an exchange (ghost mode): the
+        slab's layers plus the layer above (its upper interface plane is owned here)."""
+        return self.k0, min(self.k1 + 1, self.n[2])
+
+    @property
     def owned_rows(self) -> tuple[int, int]:
         """Rows this rank owns (interface planes belong to the lower rank)."""
         return (self.row_begin + (self.plane if self.rank > 0 else 0), self.row_end)
@@ -228,10 +234,17 @@ class SlabProblem:
     cube, E = E_range[global cell % 200], nu = 0.3, x = 0 clamped, x = 1 prescribed; form
     "linear" (elasticity, the reference J at d = 0) or "neo" (neo-Hookean, device AD tangent at
     u = 1e-3 sin(pi x)). ``assemble()`` = local gather assembly + interface exchange;
-    ``assemble_residual()`` = the reference's setF sequence on the slab with the ghost update."""
+    ``assemble_residual()`` = the reference's setF sequence on the slab with the ghost update.
+
+    mode "exchange" (default, the RCCL path) or "ghost": the communication-free alternative of
+    SURVEY §8(e) (dolfinx GhostMode.shared_facet, doc.tex:448-453) -- the rank also assembles the
+    cell layer above its slab, so the rows it owns (its upper interface plane included) are complete
+    without any exchange, at the price of one redundant layer of cells; its matrix window is its
+    owned rows only. ``assemble_residual`` is exchange-mode only."""
 
     def __init__(self, n: int, rank: int, world: int, device, degree: int = 2, nu: float = 0.3, groups=None,
-                 cell_type=None, exchange: str = "suffix", form: str = "linear", qdeg: int | None = None):
+                 cell_type=None, exchange: str = "suffix", form: str = "linear", qdeg: int | None = None,
+                 mode: str = "exchange"):
         from . import fem, mesh
         from .la import MatrixCSR
         from .materials import e_range
@@ -241,7 +254,12 @@ class SlabProblem:
         self.part = part
         L = (1.0, 1.0, 1.0)
         m_pat = mesh.create_box(L, (n, n, n), ct, device=device, z_range=(part.kp0, part.kp1))
-        m_asm = mesh.create_box(L, (n, n, n), ct, device=device, z_range=(part.k0, part.k1))
+        if mode not in ("exchange", "ghost"):
+            raise ValueError(f"unknown slab mode {mode}")
+        self.mode = mode
+        # ghost mode: cells of the layer above the slab too (complete rows on the upper plane)
+        zr = part.assembly_layers if mode == "ghost" else (part.k0, part.k1)
+        m_asm = mesh.create_box(L, (n, n, n), ct, device=device, z_range=zr)
         nloc = part.num_local_nodes
         dof_pat = part.to_local(fem._structured_dofmap(m_pat, degree)[0])
         dof_asm = part.to_local(fem._structured_dofmap(m_asm, degree)[0])
@@ -252,7 +270,8 @@ class SlabProblem:
         del xs
         a_pat = fem.LinearElasticity(V_pat, E=1.0, nu=nu)
         pat = fem.create_matrix(a_pat)
-        self.A = MatrixCSR(pat.indptr, pat.indices, 3, window=(part.row_begin, part.row_end))
+        win = part.owned_rows if mode == "ghost" else (part.row_begin, part.row_end)
+        self.A = MatrixCSR(pat.indptr, pat.indices, 3, window=win)
         V_pat._adjacency = None  # the pattern's adjacency is not needed after create_matrix
         cells_per_layer = n * n * (6 if ct == mesh.CellType.tetrahedron else 1)
         cid = torch.arange(m_asm.num_cells, device=device, dtype=torch.int64) + part.k0 * cells_per_layer
@@ -270,6 +289,15 @@ class SlabProblem:
         self.bcs = [fem.dirichletbc(0.0, left, V), fem.dirichletbc([0.01, 0.0, 0.0], right, V)]
         marker, _ = fem._combine_bcs(V, self.bcs)
         self.V = V
+        self.num_cells = n * n * (part.k1 - part.k0) * (6 if ct == mesh.CellType.tetrahedron else 1)
+        self.num_cells_assembled = m_asm.num_cells
+        if mode == "ghost":
+            self.split, self.n_iface, self.slices, self.suffix, self.fixups = None, 0, {}, None, None
+            self.exchange_bytes = 0
+            self.groups = groups
+            self.kernel_name = ("k_cell_records + k_gather over the owned rows, cells of the slab and the "
+                                "layer above (no exchange)")
+            return
         # rows in three kinds of range: the interface planes (assembled first, then exchanged
         # while the interior rows assemble) and the interior
         iface = [rr for rr in (part.lower, part.upper) if rr is not None]
@@ -286,13 +314,18 @@ class SlabProblem:
         self.exchange_bytes = 8 * bs2 * nblk  # values all-reduced per assembly by this rank
         self.fixups = bc_diagonal_fixups(part, self.A.indptr, self.A.indices, marker, 3)
         self.groups = groups if groups is not None else make_pair_groups(world)
-        self.num_cells = m_asm.num_cells
         self.kernel_name = ("k_cell_records + k_gather (interface planes, then interior rows) "
                             "+ 2-rank all_reduce(SUM) per slab boundary overlapping the interior rows")
 
     def assemble(self, overlap: bool = True):
         """Records of all cells; the interface-plane rows; their 2-rank all-reduces issued on
-        RCCL's stream; the interior rows on the compute stream meanwhile; wait; bc diagonals."""
+        RCCL's stream; the interior rows on the compute stream meanwhile; wait; bc diagonals.
+        (ghost mode: one gather over the owned rows, nothing exchanged.)"""
+        if self.mode == "ghost":
+            from . import fem
+
+            fem.assemble_matrix(self.a, bcs=self.bcs, A=self.A)
+            return
         sg = self.split
         sg.prepare()
         for i in range(self.n_iface):
@@ -314,6 +347,8 @@ class SlabProblem:
         local dof vector [num_local_nodes * 3]: owned rows complete, interface copies consistent."""
         from . import fem
 
+        if self.mode != "exchange":
+            raise NotImplementedError("assemble_residual: exchange mode")
         V, a = self.V, self.a
         if b is None:
             b = torch.zeros(V.num_dofs, dtype=torch.float64, device=V.mesh.device)

@@ -111,3 +111,39 @@ def test_slab_residual_gpu_gloo(world, n, kind):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     mp.spawn(_residual_worker, args=(world, _port(), n, kind), nprocs=world, join=True)
+
+
+@pytest.mark.parametrize("world,n,kind", [(2, 6, "linear"), (3, 7, "neo")])
+def test_slab_ghost_mode_gpu(world, n, kind):
+    """SlabProblem(mode="ghost"): no exchange; each rank's owned rows (HIP gather over its slab plus
+    the layer above) equal the single-process full-mesh GPU assembly. The ranks need no
+    communication, so they run one after the other in this process."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import sys
+
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "fem-libraries_amd"))
+    import bench
+    from femasm import fem, parallel
+
+    dev = torch.device("cuda", 0)
+    m, V, a, bcs = bench.build_problem(n, dev, cfg=bench.CONFIGS["Eneo" if kind == "neo" else "E"])
+    A = fem.assemble_matrix(a, bcs=bcs)
+    ip_g, ix_g, vg = A.indptr.cpu().numpy(), A.indices.cpu().numpy(), A.data.cpu().numpy()
+    scale = np.abs(vg).max()
+    for rank in range(world):
+        prob = parallel.SlabProblem(n, rank, world, dev, form=kind, mode="ghost")
+        prob.assemble()
+        torch.cuda.synchronize()
+        part = prob.part
+        r0, r1 = part.owned_rows
+        assert prob.A.parts[0][:2] == (r0, r1) and prob.exchange_bytes == 0
+        ip_l, ix_l = prob.A.indptr.cpu().numpy(), prob.A.indices.cpu().numpy()
+        vl = prob.A.parts[0][2].cpu().numpy()
+        w0 = ip_l[r0]
+        for r in range(r0, r1):
+            g = r + part.node_offset
+            assert np.array_equal(ix_l[ip_l[r]:ip_l[r + 1]] + part.node_offset, ix_g[ip_g[g]:ip_g[g + 1]])
+            err = np.abs(vl[ip_l[r] - w0:ip_l[r + 1] - w0] - vg[ip_g[g]:ip_g[g + 1]]).max()
+            assert err <= 1e-12 * scale, f"rank {rank} row {r}: rel err {err / scale:.2e}"

@@ -206,3 +206,48 @@ def test_slab_partition_covers_all_layers():
         # owned rows tile the global lattice exactly once
         owned = sum(p.owned_rows[1] - p.owned_rows[0] for p in parts)
         assert owned == (2 * n + 1) ** 3
+
+
+@pytest.mark.parametrize("world,n,kind", [(2, 4, "linear"), (3, 5, "linear"), (2, 4, "neo")])
+def test_slab_ghost_mode_rows_complete(world, n, kind):
+    """The communication-free slab mode (SlabProblem(mode="ghost"), SURVEY §8(e) alternative): each
+    rank assembles the cells of SlabPartition.assembly_layers (its layers + the one above) and its
+    owned rows equal the global assembly with no exchange at all (oracle per rank)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "fem-libraries_amd"))
+    sys.path.insert(0, ROOT)
+    from femasm import fem, mesh, parallel
+    from femasm.materials import e_range
+    from oracle import oracle as O
+
+    p, bs, L, ct = 2, 3, (1.0, 1.0, 1.0), mesh.CellType.tetrahedron
+    m = mesh.create_unit_cube(n, n, n, ct)
+    dof = fem._structured_dofmap(m, p)[0].numpy()
+    gip, gix = O.sparsity(dof, (p * n + 1) ** 3)
+    gx = fem._structured_node_coordinates(m, p)
+    glam, gmu = O.lame(e_range()[np.arange(m.num_cells) % 200], 0.3)
+    gvals = _assemble(O, kind, p, dof, m.cells.numpy(), m.x.numpy(), glam, gmu, _state(gx, kind), gip, gix,
+                      _bc_marker(gx, bs).numpy())
+    scale = np.abs(gvals).max()
+    covered = 0
+    for rank in range(world):
+        part = parallel.SlabPartition((n, n, n), p, rank, world)
+        m_pat = mesh.create_box(L, (n, n, n), ct, z_range=(part.kp0, part.kp1))
+        m_asm = mesh.create_box(L, (n, n, n), ct, z_range=part.assembly_layers)
+        nloc = part.num_local_nodes
+        ip, ix = O.sparsity(part.to_local(fem._structured_dofmap(m_pat, p)[0]).numpy(), nloc)
+        dof_asm = part.to_local(fem._structured_dofmap(m_asm, p)[0]).numpy()
+        xl = fem._structured_node_coordinates(m_asm, p)[part.node_offset:part.node_offset + nloc]
+        cid = np.arange(m_asm.num_cells) + part.k0 * n * n * 6
+        lam, mu = O.lame(e_range()[cid % 200], 0.3)
+        vals = _assemble(O, kind, p, dof_asm, m_asm.cells.numpy(), m_asm.x.numpy(), lam, mu, _state(xl, kind), ip,
+                         ix, _bc_marker(xl, bs).numpy())
+        r0, r1 = part.owned_rows
+        for r in range(r0, r1):
+            g = r + part.node_offset
+            assert np.array_equal(ix[ip[r]:ip[r + 1]] + part.node_offset, gix[gip[g]:gip[g + 1]])
+            err = np.abs(vals[ip[r]:ip[r + 1]] - gvals[gip[g]:gip[g + 1]]).max()
+            assert err <= 1e-12 * scale, f"rank {rank} row {r}: rel err {err / scale:.2e}"
+        covered += r1 - r0
+    assert covered == (p * n + 1) ** 3  # the owned rows partition the global rows
