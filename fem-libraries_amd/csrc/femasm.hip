@@ -3066,6 +3066,9 @@ __global__ void k_plan_colors_stats(const int64_t* __restrict__ row_start, const
 #ifndef FA_P2TET_NSPLIT
 #define FA_P2TET_NSPLIT 2  // measured best with the reference-tensor blocks (n=120 sweep)
 #endif
+#ifndef FA_P1TET_NSPLIT
+#define FA_P1TET_NSPLIT 1  // P1 tetrahedra: whole entries (4 blocks per item); config C 1.86 vs 1.97 ms (2), 2.25 (4)
+#endif
 static int lin_simplex_nsplit(int ct, int p, int nq, bool affine = false) {
   // affine hexahedra (MAT_AFFT): Q1 / Q2 / Q3 with their default rules
   if (affine && ct == FA_HEXAHEDRON && p == 1 && nq == 8) return 2;
@@ -3076,7 +3079,7 @@ static int lin_simplex_nsplit(int ct, int p, int nq, bool affine = false) {
   if (affine && ct == FA_QUADRILATERAL && p == 3 && nq == 16) return 4;
   if (ct == FA_TRIANGLE && p == 1 && nq == 1) return 1;
   if (ct == FA_TRIANGLE && p == 2 && nq == 3) return 2;
-  if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return 2;
+  if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return FA_P1TET_NSPLIT;
   if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return FA_P2TET_NSPLIT;
   return 0;
 }
@@ -3711,7 +3714,7 @@ static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const
   if (lin_uniform_nu(P.F)) {
     if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, MAT_LINU>(P, bc, s, W);
     if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, MAT_LINU>(P, bc, s, W);
-    if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, MAT_LINU>(P, bc, s, W);
+    if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, FA_P1TET_NSPLIT, MAT_LINU>(P, bc, s, W);
     if (ct == FA_TETRAHEDRON && p == 2 && nq == 4)
       return launch_gather<3, 10, 4, 4, FA_P2TET_NSPLIT, MAT_LINU>(P, bc, s, W);
   }
