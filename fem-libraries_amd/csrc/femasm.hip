@@ -3066,16 +3066,26 @@ __global__ void k_plan_colors_stats(const int64_t* __restrict__ row_start, const
 #ifndef FA_P2TET_NSPLIT
 #define FA_P2TET_NSPLIT 2  // measured best with the reference-tensor blocks (n=120 sweep)
 #endif
+// affine tensor cells: column nodes per item = NN / NSPLIT
+#ifndef FA_Q2HEX_NSPLIT
+#define FA_Q2HEX_NSPLIT 9
+#endif
+#ifndef FA_Q3HEX_NSPLIT
+#define FA_Q3HEX_NSPLIT 32
+#endif
+#ifndef FA_Q2QUAD_NSPLIT
+#define FA_Q2QUAD_NSPLIT 3
+#endif
 #ifndef FA_P1TET_NSPLIT
 #define FA_P1TET_NSPLIT 1  // P1 tetrahedra: whole entries (4 blocks per item); config C 1.86 vs 1.97 ms (2), 2.25 (4)
 #endif
 static int lin_simplex_nsplit(int ct, int p, int nq, bool affine = false) {
   // affine hexahedra (MAT_AFFT): Q1 / Q2 / Q3 with their default rules
   if (affine && ct == FA_HEXAHEDRON && p == 1 && nq == 8) return 2;
-  if (affine && ct == FA_HEXAHEDRON && p == 2 && nq == 27) return 9;
-  if (affine && ct == FA_HEXAHEDRON && p == 3 && nq == 64) return 32;
+  if (affine && ct == FA_HEXAHEDRON && p == 2 && nq == 27) return FA_Q2HEX_NSPLIT;
+  if (affine && ct == FA_HEXAHEDRON && p == 3 && nq == 64) return FA_Q3HEX_NSPLIT;
   if (affine && ct == FA_QUADRILATERAL && p == 1 && nq == 4) return 1;
-  if (affine && ct == FA_QUADRILATERAL && p == 2 && nq == 9) return 3;
+  if (affine && ct == FA_QUADRILATERAL && p == 2 && nq == 9) return FA_Q2QUAD_NSPLIT;
   if (affine && ct == FA_QUADRILATERAL && p == 3 && nq == 16) return 4;
   if (ct == FA_TRIANGLE && p == 1 && nq == 1) return 1;
   if (ct == FA_TRIANGLE && p == 2 && nq == 3) return 2;
@@ -3114,8 +3124,11 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   const bool stats_col = ev && ev[0] == '1' && ev[1] == 'c';              // FA_ORDER_STATS=1c
   const char* ke = getenv("FEMASM_ORDER_KICKS");
   const int kicks = ke ? atoi(ke) : FA_ORDER_KICKS;
-  // positional plan: the plain map is copied aside (the order kernel rewrites by position)
-  const bool posn = eadj != nullptr && 16 % ns == 0;
+  // positional plan: the plain map is copied aside (the order kernel rewrites by position). Only
+  // for the kernels that read one (k_gather's POSM: an entry's items fill whole 16-lane quarters,
+  // and affine tensor cells only with a full bc mask, NN * GD <= 32)
+  const bool tensor = mesh->cell_type == FA_HEXAHEDRON || mesh->cell_type == FA_QUADRILATERAL;
+  const bool posn = eadj != nullptr && 16 % ns == 0 && !(tensor && mesh->nn * mesh->gdim > 32);
   uint16_t *src = nullptr, *eperm = nullptr;
   const int64_t nent = mesh->ncells * mesh->nn;
   if (posn) {
@@ -3143,10 +3156,10 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   else if (mesh->nn == 10 && ns == 5) ORD(10, 5);
   else if (mesh->nn == 10 && ns == 1) ORD(10, 1);
   else if (mesh->nn == 8 && ns == 2) ORD(8, 2);
-  else if (mesh->nn == 27 && ns == 9) ORD(27, 9);
-  else if (mesh->nn == 64 && ns == 32) ORD(64, 32);
+  else if (mesh->nn == 27 && ns == FA_Q2HEX_NSPLIT) ORD(27, FA_Q2HEX_NSPLIT);
+  else if (mesh->nn == 64 && ns == FA_Q3HEX_NSPLIT) ORD(64, FA_Q3HEX_NSPLIT);
   else if (mesh->nn == 4 && ns == 1) ORD(4, 1);
-  else if (mesh->nn == 9 && ns == 3) ORD(9, 3);
+  else if (mesh->nn == 9 && ns == FA_Q2QUAD_NSPLIT) ORD(9, FA_Q2QUAD_NSPLIT);
   else if (mesh->nn == 16 && ns == 4) ORD(16, 4);
   else ok = false;
 #undef ORD
@@ -3536,6 +3549,15 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     P.slot_order = 0;
     P.eadj = nullptr;
   }
+  // a positional plan's slot map is by position: a kernel without positional items (k_gather's
+  // POSM) cannot read it -- search the slots in LDS instead
+  constexpr bool POSM_K = (MAT == 0 || MAT == MAT_LINU || (MAT == MAT_AFFT && NN * GD <= 32)) && R::SIMP &&
+                          NN % NSPLIT == 0;
+  if (P.eadj && !POSM_K) {
+    P.slots = nullptr;
+    P.slot_order = 0;
+    P.eadj = nullptr;
+  }
   static_assert(NN * GD <= 32 || MAT == MAT_AFFT, "bc mask holds 32 dofs");
   if (P.plan_maxb > gather_maxb(MAT == FA_NEO_HOOKEAN, GD * GD))
     return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, this form's kernel %d: plan with fa_plan_gather_form",
@@ -3688,12 +3710,12 @@ static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const
     // affine hexahedra: the row gather computes every block from the cell's Jacobian and the 1-D
     // matrices (MAT_AFFT); the MFMA element kernel + block store serves general trilinear cells
     if (m->degree == 1 && T.nq == 8) return launch_gather<3, 8, 8, 8, 2, MAT_AFFT>(P, bc, s, W);
-    if (m->degree == 2 && T.nq == 27) return launch_gather<3, 27, 8, 27, 9, MAT_AFFT>(P, bc, s, W);
-    if (m->degree == 3 && T.nq == 64) return launch_gather<3, 64, 8, 64, 32, MAT_AFFT>(P, bc, s, W);
+    if (m->degree == 2 && T.nq == 27) return launch_gather<3, 27, 8, 27, FA_Q2HEX_NSPLIT, MAT_AFFT>(P, bc, s, W);
+    if (m->degree == 3 && T.nq == 64) return launch_gather<3, 64, 8, 64, FA_Q3HEX_NSPLIT, MAT_AFFT>(P, bc, s, W);
   }
   if (m->cell_type == FA_QUADRILATERAL && kind == FA_LINEAR_ELASTICITY && P.affine && lin_uniform_nu(P.F)) {
     if (m->degree == 1 && T.nq == 4) return launch_gather<2, 4, 4, 4, 1, MAT_AFFT>(P, bc, s, W);
-    if (m->degree == 2 && T.nq == 9) return launch_gather<2, 9, 4, 9, 3, MAT_AFFT>(P, bc, s, W);
+    if (m->degree == 2 && T.nq == 9) return launch_gather<2, 9, 4, 9, FA_Q2QUAD_NSPLIT, MAT_AFFT>(P, bc, s, W);
     if (m->degree == 3 && T.nq == 16) return launch_gather<2, 16, 4, 16, 4, MAT_AFFT>(P, bc, s, W);
   }
   if (m->cell_type == FA_HEXAHEDRON && kind == FA_LINEAR_ELASTICITY) {
