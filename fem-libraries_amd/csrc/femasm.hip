@@ -998,6 +998,10 @@ struct GatherArgs {
   const double* rec;  // [ncells][Rec::SIZE]
   const uint32_t* bcmask;  // [ncells] or NULL
   int* err;
+  // contribution plan (fa_plan_contrib, k_gather_own) or NULL
+  const int64_t* cw;       // [nchunks + 1] offsets of the chunks' word sections (u16 units)
+  const int32_t* ccells;   // [nchunks][FA_OWN_CCAP] the chunk's distinct cells (-1 padded)
+  const uint16_t* cwords;  // per chunk: 256 lane starts, then K x 256 contribution words
 };
 
 template <int GD, int NN, int NV, int NQ, int MAT>
@@ -2474,6 +2478,264 @@ void k_gather(GatherArgs P) {
 #endif
 }
 
+// ------------------------------------------------------------------------------ block-owner gather
+// k_gather_own: the uniform-nu affine-simplex gather (MAT_LINU) without per-contribution LDS
+// atomics. The contribution plan (fa_plan_contrib) lists, per chunk, every (cell, row node a,
+// column node b) contribution sorted by destination block and cut into 256 equal lane segments
+// (K per lane). A lane sums its segment's contributions to one block in registers and writes the
+// block once, with a plain LDS store, at the block's last contribution; a lane whose segment ends
+// inside a block adds that partial sum with one LDS atomic after a barrier (about half of the
+// lanes, once per chunk). The chunk's distinct cells' records are staged in LDS once per chunk
+// (one 80-B load per cell instead of one per item), the reference-tensor table B_ab sits in LDS.
+// Output: the chunk is streamed to HBM with coalesced 16-B stores, exactly as k_gather does.
+#ifndef FA_OWN_LDS
+#define FA_OWN_LDS 28672  // output staging bytes per workgroup
+#endif
+#ifndef FA_OWN_CCAP
+#define FA_OWN_CCAP 128  // distinct cells (and adjacency entries) per chunk of a contribution plan
+#endif
+#ifndef FA_OWN_WAVES
+#define FA_OWN_WAVES 3
+#endif
+// timing-only ablations of k_gather_own (wrong results): 1 no block writes (flush), 2 no table
+// reads, 3 no record reads, 4 no contribution loop (staging + store skeleton)
+#ifndef FA_OWN_ABL
+#define FA_OWN_ABL 0
+#endif
+__host__ __device__ constexpr int own_maxb(int bs2) { return FA_OWN_LDS / (8 * bs2) < 1023 ? FA_OWN_LDS / (8 * bs2) : 1023; }
+// contribution word (u16): bits 0-7 cell slot, 8-14 a * NN + b (127: padding), 15 last of its block
+constexpr uint32_t kOwnPad = 0x7F00u;
+constexpr uint32_t kOwnIdle = 0xFFFFu;  // lane start of a lane with no contribution
+
+template <int GD, int NN>
+__global__ __launch_bounds__(256, FA_OWN_WAVES) void k_gather_own(GatherArgs P) {
+  using R = Rec<GD, GD + 1, 1, MAT_LINU>;
+  constexpr int BS2 = GD * GD, MAXB = own_maxb(BS2), NAB = NN * NN, RS = R::SIZE, CCAP = FA_OWN_CCAP;
+  constexpr int KMAX = (CCAP * NN + 255) / 256;
+  static_assert(NAB < 127 && CCAP <= 256 && NN * GD <= 32, "contribution word / bc mask");
+  __shared__ __attribute__((aligned(16))) double s_out[MAXB * BS2 + 2];
+  __shared__ __attribute__((aligned(16))) double s_rec[CCAP * RS];
+  __shared__ uint32_t s_mask[CCAP];
+  __shared__ double s_tab[NAB * BS2];
+  __shared__ uint16_t s_wd[KMAX * 256 + 256];  // lane starts, then the words [k][lane]
+  __shared__ int32_t s_cell[CCAP];             // cells of the chunk after the next one
+  const int tid = threadIdx.x;
+  for (int t = tid; t < NAB * BS2; t += 256) s_tab[t] = P.ahat[t];
+  const int64_t abase = sload(P.A.indptr, P.A.row_begin);
+  const int64_t per = (P.nchunks + 7) / 8;
+  // XCD-aware order (as k_gather): workgroup b walks XCD (b % 8)'s contiguous chunk range
+  auto chunk_of = [&](int64_t v) -> int64_t {
+    if (v >= 8 * per) return P.nchunks;
+    const int64_t c = (v % 8) * per + v / 8;
+    return c < P.nchunks ? c : P.nchunks;
+  };
+  auto nwords = [&](int64_t cc) -> int { return (int)((sload(P.cw, cc + 1) - sload(P.cw, cc)) >> 8) - 1; };
+  // Prefetch registers of the next chunk: its lane program and its cells' records. They are
+  // loaded at the top of a chunk and staged to LDS after that chunk's blocks are computed and
+  // BEFORE its store, so waiting for them never also waits for the chunk's stores (vmcnt counts
+  // stores); the compute phase reads LDS only.
+  uint32_t pw[KMAX + 1];
+  double pr[RS];
+  uint32_t pm = 0u;
+  int32_t pcell = -1, pcell2 = -1;
+  auto fetch = [&](int64_t cc, int32_t cell) {
+    const int K = nwords(cc);
+    const uint16_t* wp = P.cwords + sload(P.cw, cc);
+    pw[0] = wp[tid];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) pw[k + 1] = k < K ? (uint32_t)wp[256 + k * 256 + tid] : kOwnPad;
+    pcell = cell;
+    if (cell >= 0) {
+      const double2* rp = reinterpret_cast<const double2*>(P.rec + (int64_t)cell * RS);
+#pragma unroll
+      for (int q = 0; q < RS / 2; ++q) {
+        const double2 t = rp[q];
+        pr[2 * q] = t.x;
+        pr[2 * q + 1] = t.y;
+      }
+      pm = P.bcmask ? P.bcmask[cell] : 0u;
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int k = 0; k <= KMAX; ++k) s_wd[k * 256 + tid] = (uint16_t)pw[k];
+    if (tid < CCAP && pcell >= 0) {
+      double2* dp = reinterpret_cast<double2*>(s_rec + tid * RS);
+#pragma unroll
+      for (int q = 0; q < RS / 2; ++q) dp[q] = make_double2(pr[2 * q], pr[2 * q + 1]);
+      s_mask[tid] = pm;
+    }
+    if (tid < CCAP) s_cell[tid] = pcell2;
+  };
+  int64_t v = blockIdx.x;
+  int64_t c = chunk_of(v);
+  if (c >= P.nchunks) return;
+  int64_t c1 = chunk_of(v + gridDim.x);
+  fetch(c, tid < CCAP ? P.ccells[c * CCAP + tid] : -1);
+  pcell2 = (tid < CCAP && c1 < P.nchunks) ? P.ccells[c1 * CCAP + tid] : -1;
+  stage();
+  __syncthreads();
+  for (;;) {
+    const int64_t c2 = chunk_of(v + 2 * gridDim.x);
+    const int K = nwords(c);
+    // the next chunk's program and records (its cells were staged last chunk), the cells of the one after
+    if (c1 < P.nchunks) fetch(c1, tid < CCAP ? s_cell[tid] : -1);
+    pcell2 = (tid < CCAP && c2 < P.nchunks) ? P.ccells[c2 * CCAP + tid] : -1;
+
+    // acc sums H = sum_c sign_c (s Ji)^T B_ab (s Ji) over the block's contributions; the trace term
+    // of K = H + tr(H) / (1 + lam/mu) I is linear, so it is added once per flush, not per contribution
+    double acc[BS2];
+#pragma unroll
+    for (int e = 0; e < BS2; ++e) acc[e] = 0.0;
+    const uint32_t start = s_wd[tid];
+    int pos = (int)(start & 1023u);
+    bool open = false;
+    uint32_t lw = 0u;  // the last word summed (its cell's mask gives the block's constrained dofs)
+    auto finish = [&](bool head) {
+      double tr = acc[0];
+#pragma unroll
+      for (int i = 1; i < GD; ++i) tr += acc[i * GD + i];
+      tr *= P.trc;
+#pragma unroll
+      for (int i = 0; i < GD; ++i) acc[i * GD + i] += tr;
+      const int cs = (int)(lw & 255u), ab = (int)((lw >> 8) & 127u);
+      const int a = ab / NN, b = ab - a * NN;
+      const uint32_t m = s_mask[cs];
+      const uint32_t lrow = (m >> (a * GD)) & ((1u << GD) - 1), lcol = (m >> (b * GD)) & ((1u << GD) - 1);
+      if (lrow | lcol) {
+#pragma unroll
+        for (int i = 0; i < GD; ++i)
+#pragma unroll
+          for (int k = 0; k < GD; ++k)
+            if (((lrow >> i) | (lcol >> k)) & 1u) acc[i * GD + k] = 0.0;
+        if (head && a == b) {  // dolfinx set_diagonal on the constrained dofs of a diagonal block
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+            if ((lrow >> i) & 1u) acc[i * GD + i] = P.diag;
+        }
+      }
+    };
+    if (start != kOwnIdle && FA_OWN_ABL != 4) {
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        if (k < K) {  // wave-uniform
+          const uint32_t w = s_wd[256 + k * 256 + tid];
+          const int ab0 = (int)((w >> 8) & 127u);
+          const bool valid = ab0 < NAB;  // padding: the tail of the last active lane
+          const int ab = valid ? ab0 : 0;
+          const int cs = valid ? (int)(w & 255u) : 0;
+          double r[RS];
+          if (FA_OWN_ABL == 3) {
+#pragma unroll
+            for (int q = 0; q < RS; ++q) r[q] = 0.5 + 0.01 * q + 1e-3 * cs;
+            r[BS2] = 1.0;
+          } else {
+            const double2* rp = reinterpret_cast<const double2*>(s_rec + cs * RS);
+#pragma unroll
+            for (int q = 0; q < RS / 2; ++q) {
+              const double2 t = rp[q];
+              r[2 * q] = t.x;
+              r[2 * q + 1] = t.y;
+            }
+          }
+#if FA_OWN_ABL == 2
+          double Ahr[BS2];
+#pragma unroll
+          for (int e = 0; e < BS2; ++e) Ahr[e] = 0.1 * e + 0.01 * ab;
+          const double* Ah = Ahr;
+#else
+          const double* Ah = s_tab + ab * BS2;
+#endif
+          double T[GD][GD];  // T = B_ab (s Ji)
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int d = 0; d < GD; ++d) {
+              double t = Ah[i * GD] * r[d];
+#pragma unroll
+              for (int kk = 1; kk < GD; ++kk) t = fma(Ah[i * GD + kk], r[kk * GD + d], t);
+              T[i][d] = t;
+            }
+          const double sg = valid ? r[BS2] : 0.0;  // sign of mu |J|; 0 drops a padding word
+          if (__any(sg != 1.0)) {                  // rare: an inverted cell or padding in the wave
+#pragma unroll
+            for (int i = 0; i < GD; ++i)
+#pragma unroll
+              for (int d = 0; d < GD; ++d) T[i][d] *= sg;
+          }
+#pragma unroll
+          for (int e = 0; e < GD; ++e)
+#pragma unroll
+            for (int d = 0; d < GD; ++d) {
+              double g = acc[e * GD + d];
+#pragma unroll
+              for (int i = 0; i < GD; ++i) g = fma(r[i * GD + e], T[i][d], g);
+              acc[e * GD + d] = g;
+            }
+          if (valid) {
+            open = true;
+            lw = w;
+            if (w & 0x8000u) {  // the block's last contribution: this lane writes it (once, plain)
+              finish(true);
+              double* o = s_out + pos * BS2;
+#pragma unroll
+              for (int e = 0; e < BS2; ++e) {
+                if (FA_OWN_ABL != 1 || acc[e] == 1.2345e-300) o[e] = acc[e];
+                acc[e] = 0.0;
+              }
+              ++pos;
+              open = false;
+            }
+          }
+        }
+      }
+    }
+    if (open) finish(false);
+    __syncthreads();  // every block's plain write is done; s_rec / s_wd / s_mask are free
+    if (open) {       // the segment ended inside a block: add the partial sum
+      double* o = s_out + pos * BS2;
+#pragma unroll
+      for (int e = 0; e < BS2; ++e) atomicAdd(o + e, acc[e]);
+    }
+    if (c1 < P.nchunks) stage();
+    __syncthreads();
+    {
+      const int64_t b0 = sload(P.chunk_b, c), b1 = sload(P.chunk_b, c + 1);
+      const int64_t off = (b0 - abase) * BS2;
+      double* out = P.A.data + off;
+      const int nv = (int)(b1 - b0) * BS2;
+      const int h = (int)(off & 1);
+      if (h && tid == 0) out_store(s_out[0], out);
+      const int np = (nv - h) >> 1;
+      typedef double dv2 __attribute__((ext_vector_type(2)));
+      dv2* out2 = reinterpret_cast<dv2*>(out + h);
+      constexpr int SU = FA_GATHER_SU;
+      for (int t0 = tid; t0 < np; t0 += 256 * SU) {
+        dv2 vv[SU];
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          const int t = t0 + 256 * u;
+          if (t < np) {
+            if (h) { vv[u].x = s_out[1 + 2 * t]; vv[u].y = s_out[2 + 2 * t]; }
+            else vv[u] = reinterpret_cast<const dv2*>(s_out)[t];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          const int t = t0 + 256 * u;
+          if (t < np) out_store(vv[u], out2 + t);
+        }
+      }
+      if (((nv - h) & 1) && tid == 0) out_store(s_out[nv - 1], out + nv - 1);
+    }
+    if (c1 >= P.nchunks) break;
+    __syncthreads();  // the store has read s_out
+    c = c1;
+    c1 = c2;
+    v += gridDim.x;
+  }
+}
+
 // ------------------------------------------------------------------------------------ adjacency
 __global__ void k_iota(int32_t* v, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -3288,6 +3550,7 @@ static int plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bs
   plan->slot_order = 0;
   plan->eadj = nullptr;
   plan->corder = nullptr;
+  plan->contrib = nullptr;
   return FA_OK;
 }
 
@@ -3304,6 +3567,226 @@ extern "C" int fa_plan_gather_form(const fa_mesh* mesh, int32_t kind, const fa_a
   if (kind != FA_NEO_HOOKEAN) return fa_plan_gather(mesh, adj, A, row_start, plan, stream);
   return plan_gather(mesh, adj, A, row_start, plan, stream, gather_maxb(true, mesh->gdim * mesh->gdim),
                      kGatherNeoEntries);
+}
+
+// ------------------------------------------------------------------------------- contribution plan
+static inline int64_t align256(int64_t b);
+__global__ void k_chunk_desc(const int64_t* __restrict__ row_start, int64_t nchunks, const int64_t* __restrict__ indptr,
+                             const int64_t* __restrict__ adj_ptr, int64_t* __restrict__ cb, int64_t* __restrict__ ca);
+// Chunking for k_gather_own: its output staging holds own_maxb blocks and its record staging
+// FA_OWN_CCAP cells (<= adjacency entries of the chunk).
+extern "C" int fa_plan_gather_contrib(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A,
+                                      int64_t* row_start, fa_plan* plan, void* stream) {
+  if (!mesh) return fail(FA_E_ARG, "null mesh");
+  return plan_gather(mesh, adj, A, row_start, plan, stream, own_maxb(mesh->gdim * mesh->gdim), FA_OWN_CCAP);
+}
+
+// One workgroup per chunk. For entry j (row node a of cell c) and column node b: the block's
+// chunk position p (search of the column in the row's pattern) and its rank among the row's
+// earlier entries whose cell also holds that column (a deterministic order within the block);
+// counting sort by p; contribution i of the sorted list goes to lane i / K, word i % K.
+template <int NN>
+__global__ __launch_bounds__(256) void k_plan_contrib(const int32_t* __restrict__ dofmap, const int64_t* __restrict__ row_start,
+                                                      int64_t nchunks, const int64_t* __restrict__ indptr,
+                                                      const int32_t* __restrict__ indices, const int64_t* __restrict__ adj_ptr,
+                                                      const int32_t* __restrict__ adj_idx, const int64_t* __restrict__ cw,
+                                                      int32_t* __restrict__ ccells, uint16_t* __restrict__ words, int maxb,
+                                                      int* err) {
+  constexpr int CCAP = FA_OWN_CCAP, NC = CCAP * NN;
+  __shared__ int32_t s_cols[1024];
+  __shared__ int32_t s_cnt[1024], s_start[1024];
+  __shared__ int32_t s_rowoff[kGatherMaxRows + 1], s_eoff[kGatherMaxRows + 1];
+  __shared__ int32_t s_ent[CCAP], s_first[CCAP];
+  __shared__ uint8_t s_erow[CCAP], s_eslot[CCAP];
+  __shared__ int32_t s_dofs[NC];
+  __shared__ int16_t s_pos[NC], s_rank[NC], s_inv[NC];
+  __shared__ int s_nslot;
+  const int tid = threadIdx.x;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t r0 = row_start[c], r1 = row_start[c + 1];
+    const int64_t b0 = indptr[r0], b1 = indptr[r1], a0 = adj_ptr[r0], a1 = adj_ptr[r1];
+    const int nr = (int)(r1 - r0), nb = (int)(b1 - b0), na = (int)(a1 - a0);
+    if (nr > kGatherMaxRows || nb > maxb || nb > 1024 || na > CCAP) {
+      if (tid == 0) atomicOr(err, 1);
+      continue;  // uniform over the workgroup
+    }
+    const int n = na * NN;
+    const int K = (int)((cw[c + 1] - cw[c]) >> 8) - 1;
+    uint16_t* wp = words + cw[c];
+    for (int t = tid; t < nb; t += 256) {
+      s_cols[t] = indices[b0 + t];
+      s_cnt[t] = 0;
+    }
+    if (tid <= nr) {
+      s_rowoff[tid] = (int)(indptr[r0 + tid] - b0);
+      s_eoff[tid] = (int)(adj_ptr[r0 + tid] - a0);
+    }
+    if (tid < na) s_ent[tid] = adj_idx[a0 + tid];
+    __syncthreads();
+    if (tid < nr)
+      for (int j = s_eoff[tid]; j < s_eoff[tid + 1]; ++j) s_erow[j] = (uint8_t)tid;
+    for (int t = tid; t < n; t += 256) s_dofs[t] = dofmap[(int64_t)(s_ent[t / NN] / NN) * NN + t % NN];
+    if (tid < na) {  // first entry of the chunk with this entry's cell
+      const int cell = s_ent[tid] / NN;
+      int f = tid;
+      for (int j = 0; j < tid; ++j)
+        if (s_ent[j] / NN == cell) { f = j; break; }
+      s_first[tid] = f;
+    }
+    __syncthreads();
+    if (tid < na) {  // the cell's slot: distinct cells in order of first appearance
+      const int f = s_first[tid];
+      int sl = 0;
+      for (int j = 0; j < f; ++j) sl += s_first[j] == j;
+      s_eslot[tid] = (uint8_t)sl;
+      if (f == tid) ccells[c * CCAP + sl] = s_ent[tid] / NN;
+    }
+    if (tid == 0) {
+      int ns = 0;
+      for (int j = 0; j < na; ++j) ns += s_first[j] == j;
+      s_nslot = ns;
+    }
+    for (int t = tid; t < n; t += 256) {
+      const int j = t / NN, row = s_erow[j];
+      const int32_t col = s_dofs[t];
+      int p = lds_find(s_cols, s_rowoff[row], s_rowoff[row + 1], col);
+      if (p < 0) {
+        atomicOr(err, 2);
+        p = 0;
+      }
+      s_pos[t] = (int16_t)p;
+      atomicAdd(&s_cnt[p], 1);
+      int rk = 0;
+      for (int j2 = s_eoff[row]; j2 < j; ++j2)
+        for (int bb = 0; bb < NN; ++bb)
+          if (s_dofs[j2 * NN + bb] == col) { ++rk; break; }
+      s_rank[t] = (int16_t)rk;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int acc = 0;
+      for (int p = 0; p < nb; ++p) {
+        s_start[p] = acc;
+        if (s_cnt[p] == 0) atomicOr(err, 4);  // a pattern block no cell contributes to
+        acc += s_cnt[p];
+      }
+    }
+    if (tid < CCAP && tid >= s_nslot) ccells[c * CCAP + tid] = -1;
+    __syncthreads();
+    for (int t = tid; t < n; t += 256) {
+      const int p = s_pos[t], rk = s_rank[t];
+      const int i = s_start[p] + rk;
+      const int lane = i / K, k = i - lane * K;
+      const int j = t / NN, b = t % NN, a = s_ent[j] % NN;
+      const uint32_t w = (uint32_t)s_eslot[j] | ((uint32_t)(a * NN + b) << 8) | (rk == s_cnt[p] - 1 ? 0x8000u : 0u);
+      wp[256 + k * 256 + lane] = (uint16_t)w;
+      s_inv[i] = (int16_t)t;
+    }
+    for (int i = n + tid; i < K * 256; i += 256) {
+      const int lane = i / K, k = i - lane * K;
+      wp[256 + k * 256 + lane] = (uint16_t)kOwnPad;
+    }
+    __syncthreads();
+    {
+      const int i = tid * K;
+      wp[tid] = (uint16_t)(i < n ? (uint32_t)s_pos[s_inv[i]] : kOwnIdle);
+    }
+    __syncthreads();
+  }
+}
+
+// word-section offsets of a plan's chunks (u16 units): 256 lane starts + K x 256 words, K =
+// ceil(nn * entries / 256); *bytes = the whole buffer [cw | ccells | words]
+static int contrib_layout(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, const fa_plan* plan, hipStream_t s,
+                          std::vector<int64_t>& cw, int64_t* bytes) {
+  int rc = check_mesh(mesh);
+  if (rc) return rc;
+  if (!adj || !A || !plan || !plan->row_start) return fail(FA_E_ARG, "null argument");
+  const int64_t nch = plan->nchunks;
+  if (nch >= (1ll << 31)) return fail(FA_E_CAPACITY, "contribution plan: %lld chunks", (long long)nch);
+  int64_t* d = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&d, sizeof(int64_t) * 2 * (nch + 1), s));
+  k_chunk_desc<<<grid_for(nch + 1), 256, 0, s>>>(plan->row_start, nch, A->indptr, adj->ptr, d, d + nch + 1);
+  LAUNCH_CHECK();
+  std::vector<int64_t> ca(nch + 1);
+  HIP_TRY(hipMemcpyAsync(ca.data(), d + nch + 1, sizeof(int64_t) * (nch + 1), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipFreeAsync(d, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  cw.assign(nch + 1, 0);
+  for (int64_t c = 0; c < nch; ++c) {
+    const int64_t n = (ca[c + 1] - ca[c]) * mesh->nn;
+    cw[c + 1] = cw[c] + 256 * ((n + 255) / 256 + 1);
+  }
+  *bytes = align256(8 * (nch + 1)) + align256(4 * nch * (int64_t)FA_OWN_CCAP) + align256(2 * cw[nch]);
+  return FA_OK;
+}
+
+static bool contrib_element(const fa_mesh* m) {
+  return (m->cell_type == FA_TRIANGLE || m->cell_type == FA_TETRAHEDRON) && (m->degree == 1 || m->degree == 2);
+}
+
+extern "C" int fa_plan_contrib_bytes(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, const fa_plan* plan,
+                                     int64_t* bytes, void* stream) {
+  if (!bytes) return fail(FA_E_ARG, "null bytes");
+  std::vector<int64_t> cw;
+  return contrib_layout(mesh, adj, A, plan, (hipStream_t)stream, cw, bytes);
+}
+
+extern "C" int fa_plan_contrib(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, void* buf, int64_t bytes,
+                               fa_plan* plan, void* stream) {
+  int rc = check_mesh(mesh);
+  if (rc) return rc;
+  if (!plan || !buf) return fail(FA_E_ARG, "null argument");
+  plan->contrib = nullptr;
+  if (!contrib_element(mesh)) return fail(FA_E_UNSUPPORTED, "contribution plans serve P1/P2 triangles and tetrahedra");
+  const int bs2 = mesh->gdim * mesh->gdim;
+  if (plan->max_blocks > own_maxb(bs2) || plan->max_adj > FA_OWN_CCAP)
+    return fail(FA_E_CAPACITY, "plan chunks hold %d blocks / %d entries (contribution kernel: %d / %d): plan with "
+                "fa_plan_gather_contrib", plan->max_blocks, plan->max_adj, own_maxb(bs2), FA_OWN_CCAP);
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<int64_t> cw;
+  int64_t need = 0;
+  if ((rc = contrib_layout(mesh, adj, A, plan, s, cw, &need))) return rc;
+  if (bytes < need) return fail(FA_E_ARG, "contribution buffer holds %lld bytes, the plan needs %lld", (long long)bytes,
+                                (long long)need);
+  const int64_t nch = plan->nchunks;
+  char* base = static_cast<char*>(buf);
+  int64_t* dcw = reinterpret_cast<int64_t*>(base);
+  int32_t* dcells = reinterpret_cast<int32_t*>(base + align256(8 * (nch + 1)));
+  uint16_t* dwords = reinterpret_cast<uint16_t*>(base + align256(8 * (nch + 1)) + align256(4 * nch * (int64_t)FA_OWN_CCAP));
+  HIP_TRY(hipMemcpyAsync(dcw, cw.data(), sizeof(int64_t) * (nch + 1), hipMemcpyHostToDevice, s));
+  int* derr = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&derr, sizeof(int), s));
+  HIP_TRY(hipMemsetAsync(derr, 0, sizeof(int), s));
+  const int grid = (int)std::min<int64_t>(std::max<int64_t>(nch, 1), 1 << 20);
+  switch (mesh->nn) {
+    case 3: k_plan_contrib<3><<<grid, 256, 0, s>>>(mesh->cells, plan->row_start, nch, A->indptr, A->indices, adj->ptr, adj->idx, dcw, dcells, dwords, own_maxb(bs2), derr); break;
+    case 6: k_plan_contrib<6><<<grid, 256, 0, s>>>(mesh->cells, plan->row_start, nch, A->indptr, A->indices, adj->ptr, adj->idx, dcw, dcells, dwords, own_maxb(bs2), derr); break;
+    case 4: k_plan_contrib<4><<<grid, 256, 0, s>>>(mesh->cells, plan->row_start, nch, A->indptr, A->indices, adj->ptr, adj->idx, dcw, dcells, dwords, own_maxb(bs2), derr); break;
+    case 10: k_plan_contrib<10><<<grid, 256, 0, s>>>(mesh->cells, plan->row_start, nch, A->indptr, A->indices, adj->ptr, adj->idx, dcw, dcells, dwords, own_maxb(bs2), derr); break;
+    default: (void)hipFreeAsync(derr, s); return fail(FA_E_UNSUPPORTED, "contribution plan: %d nodes per cell", mesh->nn);
+  }
+  LAUNCH_CHECK();
+  int herr = 0;
+  HIP_TRY(hipMemcpyAsync(&herr, derr, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipFreeAsync(derr, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (herr) return fail(FA_E_PATTERN, "contribution plan: chunk capacity / pattern error 0x%x", herr);
+  plan->contrib = buf;
+  return FA_OK;
+}
+
+// the kernel's views of plan->contrib (NULL pointers without one)
+static void set_contrib(GatherArgs& P, const fa_plan* plan) {
+  P.cw = nullptr;
+  P.ccells = nullptr;
+  P.cwords = nullptr;
+  if (!plan || !plan->contrib) return;
+  const int64_t nch = plan->nchunks;
+  const char* base = static_cast<const char*>(plan->contrib);
+  P.cw = reinterpret_cast<const int64_t*>(base);
+  P.ccells = reinterpret_cast<const int32_t*>(base + align256(8 * (nch + 1)));
+  P.cwords = reinterpret_cast<const uint16_t*>(base + align256(8 * (nch + 1)) + align256(4 * nch * (int64_t)FA_OWN_CCAP));
 }
 
 // ------------------------------------------------------------------------------- chunk locality order
@@ -3617,6 +4100,15 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     }
 #endif
     bool launched = false;
+    if constexpr (MAT == MAT_LINU && Rec<GD, NV, NQ, MAT>::SIMP && NN * GD <= 32 && NN * NN < 127) {
+      if (P.cw) {  // contribution plan: the block-owner gather
+        if (P.plan_maxb > own_maxb(GD * GD))
+          return fail(FA_E_ARG, "contribution plan chunks hold %d blocks, the kernel %d", P.plan_maxb, own_maxb(GD * GD));
+        const int64_t go = gather_grid(k_gather_own<GD, NN>, P.nchunks);
+        k_gather_own<GD, NN><<<(unsigned)go, 256, 0, s>>>(P);
+        launched = true;
+      }
+    }
     if constexpr (MAT == MAT_LINU && Rec<GD, NV, NQ, MAT>::SIMP && Bary<GD, NN>::NPART == NSPLIT &&
                   Bary<GD, NN>::NB == (NN + NSPLIT - 1) / NSPLIT && FA_GATHER_BARY && FA_ABL == 0) {
       if (P.slots && !P.slot_order) {  // barycentric blocks read the plain slot map
@@ -3827,6 +4319,7 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr;
     P.affine = (plan->cell_flags & FA_PLAN_AFFINE) != 0;
     P.t1d = T.t1d; P.lat = T.lat;
+    set_contrib(P, plan);
     bool handled = false;
     rc = dispatch_gather(mesh, T, F.kind, P, bc, s, &handled);
     if (rc) return rc;
@@ -3902,6 +4395,7 @@ static int gather_stage(const fa_mesh* mesh, const fa_form* form, const fa_adjac
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;
+    set_contrib(P, plan);
   }
   bool handled = false;
   rc = dispatch_gather(mesh, T, F.kind, P, bc, s, &handled, W);

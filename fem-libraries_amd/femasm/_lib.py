@@ -83,6 +83,7 @@ class fa_plan(ctypes.Structure):
         ("cell_flags", ctypes.c_int32),
         ("eadj", ctypes.c_void_p),
         ("corder", ctypes.c_void_p),
+        ("contrib", ctypes.c_void_p),
     ]
 
 
@@ -101,6 +102,9 @@ SIGNATURES = {
     "fa_plan_slots": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_plan_order": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_plan_locality": (ctypes.c_int, [P, P, P, P, P]),
+    "fa_plan_gather_contrib": (ctypes.c_int, [P, P, P, P, P, P]),
+    "fa_plan_contrib_bytes": (ctypes.c_int, [P, P, P, P, P, P]),
+    "fa_plan_contrib": (ctypes.c_int, [P, P, P, P, I64, P, P]),
     "fa_tabulate_cells": (ctypes.c_int, [P, P, I64, I64, P, P]),
     "fa_assemble_matrix": (ctypes.c_int, [P, P, P, P, P, D, P, I32, P]),
     "fa_gather_work_bytes": (ctypes.c_int, [P, P, P]),

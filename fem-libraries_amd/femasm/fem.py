@@ -508,12 +508,45 @@ def _plan_locality(V, fm, adj, plan, sh):
     return corder if plan.corder else None
 
 
+def _use_contrib(V, kind) -> bool:
+    """Block-owner gather (fa_plan_contrib) for linear elasticity on P1/P2 triangles and
+    tetrahedra, opt-in with FEMASM_CONTRIB=1 (measured slower than the LDS-atomic gather on
+    configs C and E)."""
+    if os.environ.get("FEMASM_CONTRIB", "0") != "1" or kind != _lib.FA_LINEAR_ELASTICITY:
+        return False
+    return V.mesh.cell_type in (_lib.FA_TRIANGLE, _lib.FA_TETRAHEDRON) and V.degree in (1, 2)
+
+
+def _plan_contrib(V, fm, adj, fb, rs, plan, sh):
+    """Chunking + contribution plan of the block-owner gather; None (plan untouched) when a chunk
+    cannot hold a row's entries (then the caller plans the LDS-atomic gather)."""
+    L = _lib.load()
+    rc = L.fa_plan_gather_contrib(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), rs.data_ptr(),
+                                  ctypes.byref(plan), sh)
+    _lib.check(rc, "fa_plan_gather_contrib")
+    if plan.nchunks == 0:
+        return None
+    nbytes = ctypes.c_int64(0)
+    _lib.check(L.fa_plan_contrib_bytes(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), ctypes.byref(plan),
+                                       ctypes.byref(nbytes), sh), "fa_plan_contrib_bytes")
+    buf = torch.empty(max(int(nbytes.value), 16), dtype=torch.uint8, device=V.mesh.device)
+    rc = L.fa_plan_contrib(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), buf.data_ptr(), buf.numel(),
+                           ctypes.byref(plan), sh)
+    if rc != _lib.FA_OK:
+        if rc == -5:  # FA_E_CAPACITY: rows with more entries than a chunk holds
+            return None
+        _lib.check(rc, "fa_plan_contrib")
+    return buf
+
+
 def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.FA_LINEAR_ELASTICITY):
     """Row-chunk plan of the gather kernel of a form kind for one row part of A's pattern (cached
     on V). Neo-Hookean forms get their own chunking (fa_plan_gather_form); the other kinds share one."""
     plans = V.__dict__.setdefault("_plans", {})
     neo = kind == _lib.FA_NEO_HOOKEAN
-    key = (A.indptr.data_ptr(), A.parts[part][0], A.parts[part][1]) + (("neo",) if neo else ())
+    contrib = _use_contrib(V, kind)
+    key = (A.indptr.data_ptr(), A.parts[part][0], A.parts[part][1]) + (("neo",) if neo else ()) + \
+        (("contrib",) if contrib else ())
     if key not in plans:
         L = _lib.load()
         fm = V._fa_mesh()
@@ -522,6 +555,11 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.
         rs = torch.empty(A.parts[part][1] - A.parts[part][0] + 1, dtype=torch.int64, device=V.mesh.device)
         plan = _lib.fa_plan()
         sh = _lib.stream_handle(V.mesh.device)
+        if contrib:
+            buf = _plan_contrib(V, fm, adj, fb, rs, plan, sh)
+            if buf is not None:
+                plans[key] = (plan, rs, A.indptr, buf)
+                return plan
         _lib.check(L.fa_plan_gather_form(ctypes.byref(fm), int(kind), ctypes.byref(adj), ctypes.byref(fb),
                                          rs.data_ptr(), ctypes.byref(plan), sh), "fa_plan_gather_form")
         slots = eadj = None

@@ -127,6 +127,9 @@ typedef struct {
                                 `slots` is then indexed by that position, chunk-relative */
   const int32_t* corder;     /* optional device [nchunks] (fa_plan_locality): the order in which the
                                 gather visits its chunks; NULL = row order */
+  const void* contrib;       /* optional contribution plan (fa_plan_contrib): P1/P2 simplices with
+                                linear elasticity of one Poisson ratio then assemble through the
+                                block-owner gather (no per-contribution LDS atomics) */
 } fa_plan;
 
 const char* fa_last_error(void);
@@ -182,6 +185,22 @@ int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A,
  * buffer of plan->nchunks int32; on success plan->corder points to it. Any permutation assembles
  * the same matrix (each chunk owns its rows); only the re-reads of the records change. */
 int fa_plan_locality(const fa_mesh* mesh, const fa_adjacency* adj, int32_t* corder, fa_plan* plan, void* stream);
+
+/* Block-owner gather (P1/P2 triangles and tetrahedra, linear elasticity with one Poisson ratio).
+ * fa_plan_gather_contrib chunks the rows for it (like fa_plan_gather, smaller chunks: at most
+ * 128 adjacency entries). fa_plan_contrib_bytes returns the device buffer size the contribution
+ * plan of that chunking needs; fa_plan_contrib fills a caller-owned buffer of that size with
+ * every chunk's (cell, row node, column node) contributions sorted by destination block and cut
+ * into equal lane segments, and sets plan->contrib. The assembly then sums each block's
+ * contributions in registers and writes it once (replaces the same dolfinx call as
+ * fa_plan_gather: create_matrix + the cell loop of assemble_matrix,
+ * FEniCSx/mechanic2d/asym_elasto_damage_model.cc:688, :852-857). */
+int fa_plan_gather_contrib(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int64_t* row_start,
+                           fa_plan* plan, void* stream);
+int fa_plan_contrib_bytes(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, const fa_plan* plan,
+                          int64_t* bytes, void* stream);
+int fa_plan_contrib(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, void* buf, int64_t bytes,
+                    fa_plan* plan, void* stream);
 
 /* Per-cell element matrices Ae [ncells_out][nn*bs][nn*bs] (dof = node*bs + comp) for cells
  * [c0, c0+ncells_out) — the batched ufcx tabulate_tensor / AssembleElementGrad. */
