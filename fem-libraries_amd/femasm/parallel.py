@@ -119,24 +119,26 @@ def bc_diagonal_fixups(part: SlabPartition, indptr: torch.Tensor, indices: torch
     """Flat value indices (window-relative) of Dirichlet diagonal entries on interface rows."""
     if marker is None:
         return None
+    # vectorised over the planes' blocks (no per-row host round trips): the diagonal block of each
+    # row is the one whose column equals the row; rows ascending, then components
     idx = []
     base = int(indptr[part.row_begin])
     for rr in (part.lower, part.upper):
-        if rr is None:
+        if rr is None or rr[1] <= rr[0]:
             continue
-        rows = torch.arange(rr[0], rr[1], device=indptr.device)
-        m = marker.reshape(-1, bs)[rows]  # [nrows, bs]
-        hit_rows = rows[m.any(1)]
-        for r in hit_rows.tolist():
-            b, e = int(indptr[r]), int(indptr[r + 1])
-            cols = indices[b:e]
-            s = b + int(torch.nonzero(cols == r)[0, 0])
-            for i in range(bs):
-                if int(marker[r * bs + i]):
-                    idx.append((s - base) * bs * bs + i * bs + i)
+        b0, b1 = int(indptr[rr[0]]), int(indptr[rr[1]])
+        counts = indptr[rr[0] + 1:rr[1] + 1] - indptr[rr[0]:rr[1]]
+        rowid = torch.repeat_interleave(torch.arange(rr[0], rr[1], device=indptr.device), counts)
+        dpos = torch.nonzero(indices[b0:b1].to(torch.int64) == rowid).flatten()
+        if dpos.numel() != rr[1] - rr[0]:
+            raise ValueError("interface rows without a diagonal block in the pattern")
+        m = marker.reshape(-1, bs)[rowid[dpos]] != 0  # [nrows, bs]
+        k, i = torch.nonzero(m, as_tuple=True)
+        idx.append((dpos[k] + (b0 - base)) * (bs * bs) + i * (bs + 1))
     if not idx:
         return None
-    return torch.tensor(idx, dtype=torch.int64, device=indptr.device)
+    out = torch.cat(idx).to(torch.int64)
+    return out if out.numel() else None
 
 
 def exchange_interfaces(part: SlabPartition, values: torch.Tensor, slices: dict, groups, fixups=None,
