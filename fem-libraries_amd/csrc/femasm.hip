@@ -740,6 +740,8 @@ __global__ __launch_bounds__(64 * ((NN + 15) / 16) * ((NN + 15) / 16)) void k_he
   constexpr int QMAX = (NQ + 3) & ~3;
   __shared__ double phi[3][QMAX][NNP];
   __shared__ double sJ[QMAX][10];  // Ji (9) + sqrt(w |J|)
+  __shared__ uint8_t s_bcn[NN];    // MODE 2: constrained-dof bits of the cell's nodes
+  static_assert(MODE != 2 || 3 * QMAX * NNP >= NT * NT * 64 * 9, "block staging fits the phi image");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nq = NQ, nqp = QMAX;
   for (int64_t ci = blockIdx.x; ci < ncells; ci += gridDim.x) {
@@ -759,6 +761,15 @@ __global__ __launch_bounds__(64 * ((NN + 15) / 16) * ((NN + 15) / 16)) void k_he
 #pragma unroll
         for (int k = 0; k < 3; ++k) sJ[tid][i * 3 + k] = Ji[i][k];
       sJ[tid][9] = sqrt(T.wq[tid] * fabs(det));
+    }
+    if (MODE == 2 && tid < NN) {
+      uint32_t bits = 0u;
+      if (bc) {
+        const int64_t n = M.cells[c * NN + tid];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) bits |= (bc[n * 3 + i] ? 1u : 0u) << i;
+      }
+      s_bcn[tid] = (uint8_t)bits;
     }
     __syncthreads();
     for (int idx = tid; idx < nqp * NNP; idx += NTHR) {
@@ -796,6 +807,44 @@ __global__ __launch_bounds__(64 * ((NN + 15) / 16) * ((NN + 15) / 16)) void k_he
           for (int k = 0; k < 3; ++k) acc[i * 3 + k] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[k], acc[i * 3 + k], 0, 0, 0);
       }
       // D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * r
+      if constexpr (MODE == 2) {
+        // block store for the row gather, Eb[c][a][b][3][3] with bc rows / columns zeroed: the
+        // wave's 4 x 16 blocks of each r go through a wave-private slice of the (now unused) phi
+        // image and leave as contiguous 8-B-per-lane stores (512 B per instruction), instead of
+        // nine 72-B-strided stores per lane
+        __syncthreads();  // every wave is past its MFMA loop: phi is free
+        double* st = &phi[0][0][0] + wave * (64 * 9);
+        const int nbv = min(16, NN - tb * 16);  // valid column blocks of this tile
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int a = ta * 16 + (lane >> 4) + 4 * r, b = tb * 16 + (lane & 15);
+          if (a < NN && b < NN) {
+            const double tr = acc[0][r] + acc[4][r] + acc[8][r];
+            const uint32_t rm = s_bcn[a], cm = s_bcn[b];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int k = 0; k < 3; ++k) {
+                const double v = lam * acc[i * 3 + k][r] + mu * acc[k * 3 + i][r] + (i == k ? mu * tr : 0.0);
+                st[lane * 9 + i * 3 + k] = (((rm >> i) | (cm >> k)) & 1u) ? 0.0 : v;
+              }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          // row j of the 4: blocks [tb*16, tb*16 + nbv) of row a_j are contiguous in Eb
+          const int nrow = nbv * 9;
+          for (int t = lane; t < 4 * nrow; t += 64) {
+            const int j = t / nrow, off = t - j * nrow;
+            const int aj = ta * 16 + j + 4 * r;
+            if (aj < NN) Ae[((ci * NN + aj) * NN + tb * 16) * 9 + off] = st[j * 144 + off];
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int a = ta * 16 + (lane >> 4) + 4 * r, b = tb * 16 + (lane & 15);
@@ -1420,8 +1469,13 @@ __device__ __forceinline__ void out_store(const T& v, T* p) {
 #ifndef FA_GATHER_TIMING
 #define FA_GATHER_TIMING 0  // 1: per-phase shader-clock totals of the gather (measurement build)
 #endif
-#if FA_GATHER_TIMING
+#ifndef FA_OWN_TIMING
+#define FA_OWN_TIMING 0  // 1: per-phase shader-clock totals of k_gather_own (measurement build)
+#endif
+#if FA_GATHER_TIMING || FA_OWN_TIMING
 __device__ unsigned long long g_gather_timing[10];
+#endif
+#if FA_GATHER_TIMING
 #define GT_MARK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #else
 #define GT_MARK(v)
@@ -2575,6 +2629,10 @@ __global__ __launch_bounds__(256, FA_OWN_WAVES) void k_gather_own(GatherArgs P) 
   pcell2 = (tid < CCAP && c1 < P.nchunks) ? P.ccells[c1 * CCAP + tid] : -1;
   stage();
   __syncthreads();
+#if FA_OWN_TIMING
+  unsigned long long ot[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long o0 = __builtin_amdgcn_s_memtime();
+#endif
   for (;;) {
     const int64_t c2 = chunk_of(v + 2 * gridDim.x);
     const int K = nwords(c);
@@ -2691,14 +2749,28 @@ __global__ __launch_bounds__(256, FA_OWN_WAVES) void k_gather_own(GatherArgs P) 
       }
     }
     if (open) finish(false);
+#if FA_OWN_TIMING
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const unsigned long long o1 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();  // every block's plain write is done; s_rec / s_wd / s_mask are free
+#if FA_OWN_TIMING
+    const unsigned long long o2 = __builtin_amdgcn_s_memtime();
+#endif
     if (open) {       // the segment ended inside a block: add the partial sum
       double* o = s_out + pos * BS2;
 #pragma unroll
       for (int e = 0; e < BS2; ++e) atomicAdd(o + e, acc[e]);
     }
     if (c1 < P.nchunks) stage();
+#if FA_OWN_TIMING
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    const unsigned long long o3 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();
+#if FA_OWN_TIMING
+    const unsigned long long o4 = __builtin_amdgcn_s_memtime();
+#endif
     {
       const int64_t b0 = sload(P.chunk_b, c), b1 = sload(P.chunk_b, c + 1);
       const int64_t off = (b0 - abase) * BS2;
@@ -2728,12 +2800,29 @@ __global__ __launch_bounds__(256, FA_OWN_WAVES) void k_gather_own(GatherArgs P) 
       }
       if (((nv - h) & 1) && tid == 0) out_store(s_out[nv - 1], out + nv - 1);
     }
+#if FA_OWN_TIMING
+    const unsigned long long o5 = __builtin_amdgcn_s_memtime();
+    ot[0] += o1 - o0;  // prefetch issue + contribution loop
+    ot[1] += o2 - o1;  // barrier after the loop
+    ot[2] += o3 - o2;  // partial atomics + staging (waits for the prefetched loads)
+    ot[3] += o4 - o3;  // barrier before the store
+    ot[4] += o5 - o4;  // store issue
+    ot[6] += 1;
+#endif
     if (c1 >= P.nchunks) break;
     __syncthreads();  // the store has read s_out
+#if FA_OWN_TIMING
+    o0 = __builtin_amdgcn_s_memtime();
+    ot[5] += o0 - o5;  // barrier after the store
+#endif
     c = c1;
     c1 = c2;
     v += gridDim.x;
   }
+#if FA_OWN_TIMING
+  if ((tid & 63) == 0)
+    for (int k = 0; k < 8; ++k) atomicAdd(&g_gather_timing[k], ot[k]);
+#endif
 }
 
 // ------------------------------------------------------------------------------------ adjacency
@@ -4105,8 +4194,25 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
         if (P.plan_maxb > own_maxb(GD * GD))
           return fail(FA_E_ARG, "contribution plan chunks hold %d blocks, the kernel %d", P.plan_maxb, own_maxb(GD * GD));
         const int64_t go = gather_grid(k_gather_own<GD, NN>, P.nchunks);
+#if FA_OWN_TIMING
+        {
+          unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+          HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_gather_timing), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
+        }
+#endif
         k_gather_own<GD, NN><<<(unsigned)go, 256, 0, s>>>(P);
         launched = true;
+#if FA_OWN_TIMING
+        {
+          unsigned long long t[10];
+          HIP_TRY(hipMemcpyFromSymbolAsync(t, HIP_SYMBOL(g_gather_timing), sizeof(t), 0, hipMemcpyDeviceToHost, s));
+          HIP_TRY(hipStreamSynchronize(s));
+          const double n = (double)(t[6] ? t[6] : 1);
+          fprintf(stderr, "[own timing] per wave-chunk (s_memtime): loop %.0f | B2 %.0f | atomics+stage %.0f | B3 %.0f | "
+                          "store %.0f | B1 %.0f | wave-chunks %llu\n", t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n,
+                  t[5] / n, t[6]);
+        }
+#endif
       }
     }
     if constexpr (MAT == MAT_LINU && Rec<GD, NV, NQ, MAT>::SIMP && Bary<GD, NN>::NPART == NSPLIT &&
