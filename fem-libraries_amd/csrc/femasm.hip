@@ -992,6 +992,13 @@ constexpr int MAT_AFFT = 11;
 #define FA_NEO_INV 1  // neo-Hookean records: AD of the strain energy in its invariants (F + 5 scalars per
                       // point) instead of the 45-entry AD tangent per point
 #endif
+#ifndef FA_NEO_CREC
+// invariant records hold C = cof F and {W_JJ + W_J/J, W_J/J, 2 W_1} (12 doubles per point in 3-D)
+// instead of F and all five coefficients (14): the reference potential W = mu/2 (I1 - 3) - mu ln J
+// + lam/2 (ln J)^2 is linear in I1, so W_11 = W_1J = 0 and the F F^T / F C^T terms of the tangent
+// vanish identically; the gather then needs neither F nor the per-point cofactor
+#define FA_NEO_CREC 1
+#endif
 template <int GD, int NV, int NQ, int MAT>
 struct Rec {
   static constexpr bool SIMP = (NV == GD + 1) || MAT == MAT_AFFT;  // affine: one Jacobian per cell
@@ -1003,7 +1010,7 @@ struct Rec {
   // sCC, sCt, s1 (neo_energy_coeffs) from QOFF, stride QSTR; FA_NEO_INV=0: the 45-entry upper
   // triangle of dP/dF at N + 1, stride NTRI
   static constexpr int QOFF = FA_NEO_INV ? ((N + 2) & ~1) : N + 1;
-  static constexpr int QSTR = FA_NEO_INV ? ((N + 6) & ~1) : NTRI;
+  static constexpr int QSTR = FA_NEO_INV ? (FA_NEO_CREC ? ((N + 4) & ~1) : ((N + 6) & ~1)) : NTRI;
   static constexpr int RAW = MAT == MAT_BLOCKS ? 2
                              : (MAT == MAT_LINU || MAT == MAT_AFFT) ? GD * GD + 1
                              : MAT == FA_ASYM_DAMAGE ? 16
@@ -1087,6 +1094,17 @@ __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, co
         double co[5];
         neo_energy_coeffs(I1, J, lam, mu, co);
         double* o = out + R::QOFF + q * R::QSTR;
+        if constexpr (FA_NEO_CREC) {
+          double Cm[GD][GD];
+          cofactor<GD>(Fq, Cm);
+#pragma unroll
+          for (int m = 0; m < N; ++m) o[m] = Cm[m / GD][m % GD];
+#pragma unroll
+          for (int t = 0; t < 3; ++t) o[N + t] = co[2 + t];
+#pragma unroll
+          for (int t = N + 3; t < R::QSTR; ++t) o[t] = 0.0;
+          continue;
+        }
 #pragma unroll
         for (int m = 0; m < N; ++m) o[m] = Fq[m];
 #pragma unroll
@@ -1920,7 +1938,7 @@ void k_gather(GatherArgs P) {
         // loaded while this one is contracted: per column K_ab += c2 Ca Cb^T - c3 Cb Ca^T +
         // c4 (ga.gb) I [+ c0 Fa Fb^T + c1 (Fa Cb^T + Ca Fb^T)], Ca = cof(F) ga, Fa = F ga
         const double* Q0 = P.rec + c * R::SIZE + R::QOFF;
-        constexpr int NL = N + 5;
+        constexpr int NL = FA_NEO_CREC ? N + 3 : N + 5;
         double Qn[NL];
 #pragma unroll
         for (int t = 0; t < NL; ++t) Qn[t] = Q0[t];
@@ -1943,13 +1961,18 @@ void k_gather(GatherArgs P) {
             ga[d] = s_w[q] * wdet * sgd;
           }
           double Cm[GD][GD];
-          {
+          if constexpr (FA_NEO_CREC) {  // the record holds C = cof F
+#pragma unroll
+            for (int m = 0; m < N; ++m) Cm[m / GD][m % GD] = Qc[m];
+          } else {
             double Fq[N];
 #pragma unroll
             for (int m = 0; m < N; ++m) Fq[m] = Qc[m];
             cofactor<GD>(Fq, Cm);
           }
-          const double c0 = Qc[N], c1 = Qc[N + 1], c2 = Qc[N + 2], c3 = Qc[N + 3], c4 = Qc[N + 4];
+          constexpr int CO = FA_NEO_CREC ? N - 2 : N;  // index of c0 (c0, c1 absent from C records)
+          const double c0 = FA_NEO_CREC ? 0.0 : Qc[CO], c1 = FA_NEO_CREC ? 0.0 : Qc[CO + 1], c2 = Qc[CO + 2],
+                       c3 = Qc[CO + 3], c4 = Qc[CO + 4];
           double u[GD], v[GD];
 #pragma unroll
           for (int i = 0; i < GD; ++i) {
@@ -1960,7 +1983,7 @@ void k_gather(GatherArgs P) {
             v[i] = c3 * ca;
           }
           // W_11 = W_1J = 0 for this energy: the F terms only where a lane has them (wave-uniform)
-          const bool mixed = __any(c0 != 0.0 || c1 != 0.0);
+          const bool mixed = !FA_NEO_CREC && __any(c0 != 0.0 || c1 != 0.0);
           double w[GD];
           if (mixed) {
 #pragma unroll
