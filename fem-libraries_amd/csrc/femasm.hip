@@ -999,6 +999,9 @@ constexpr int MAT_AFFT = 11;
 // vanish identically; the gather then needs neither F nor the per-point cofactor
 #define FA_NEO_CREC 1
 #endif
+#ifndef FA_NEO_TILE
+#define FA_NEO_TILE 1  // neo-Hookean C records in 64-cell tiles (Rec::TILED)
+#endif
 template <int GD, int NV, int NQ, int MAT>
 struct Rec {
   static constexpr bool SIMP = (NV == GD + 1) || MAT == MAT_AFFT;  // affine: one Jacobian per cell
@@ -1017,6 +1020,18 @@ struct Rec {
                              : MAT == FA_NEO_HOOKEAN ? QOFF + NQ * QSTR
                                                      : (SIMP ? GD * GD + 3 : NQ * (GD * GD + 1) + 2);
   static constexpr int SIZE = (RAW + 1) & ~1;  // even: 16-byte aligned records
+  // neo-Hookean C records (FA_NEO_TILE): tiles of 64 cells, [64 heads][NQ][64 point records], so
+  // the records kernel stores every block of a tile contiguously (k_neo_records_tiled); a cell's
+  // head and each of its point records stay contiguous and 16-B aligned for the gather's loads
+  static constexpr bool TILED = MAT == FA_NEO_HOOKEAN && FA_NEO_INV && FA_NEO_CREC && FA_NEO_TILE;
+  static constexpr int PSTR = TILED ? 64 * QSTR : QSTR;  // stride between a cell's point records
+  __host__ __device__ static constexpr int64_t head(int64_t c) {
+    return TILED ? (c >> 6) * (64 * SIZE) + (c & 63) * QOFF : c * SIZE;
+  }
+  __host__ __device__ static constexpr int64_t point0(int64_t c) {
+    return TILED ? (c >> 6) * (64 * SIZE) + 64 * QOFF + (c & 63) * QSTR : c * SIZE + QOFF;
+  }
+  __host__ __device__ static constexpr int64_t count(int64_t nc) { return TILED ? (nc + 63) / 64 * 64 * SIZE : nc * SIZE; }
 };
 
 __host__ __device__ constexpr int tri_index(int i, int j, int n) {  // upper triangle, i <= j
@@ -1211,6 +1226,86 @@ __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, co
     }
     bcmask[c] = m;
   }
+  }
+}
+
+// Neo-Hookean C records in 64-cell tiles (Rec::TILED): one wave per tile, lane = cell. Each block
+// of the tile (the 64 heads, then each quadrature point's 64 records) is written by the lanes into
+// a wave-private LDS buffer and stored as one contiguous run with 16 B per lane, instead of every
+// lane storing its own 464-B record (one cache line per lane per store instruction).
+template <int GD, int NN, int NV, int NQ>
+__global__ __launch_bounds__(256) void k_neo_records_tiled(MeshView M, FormView F, const double* __restrict__ tab,
+                                                           const int8_t* __restrict__ bc, double* __restrict__ rec,
+                                                           uint32_t* __restrict__ bcmask) {
+  using R = Rec<GD, NV, NQ, FA_NEO_HOOKEAN>;
+  static_assert(R::TILED && R::SIMP && NN * GD <= 32, "tiled neo-Hookean records");
+  constexpr int N = R::N, QO = R::QOFF, QS = R::QSTR;
+  constexpr int BUF = 64 * (QO > QS ? QO : QS);
+  __shared__ __attribute__((aligned(16))) double sbuf[4][BUF];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* sb = sbuf[wave];
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  auto flush = [&](double* dst, int n) {  // sb[0, n) -> dst, n even, dst 16-B aligned
+    wave_sync();
+    const double2* s2 = reinterpret_cast<const double2*>(sb);
+    double2* d2 = reinterpret_cast<double2*>(dst);
+    for (int t = lane; t < n / 2; t += 64) d2[t] = s2[t];
+    wave_sync();
+  };
+  const int64_t ntiles = (M.ncells + 63) / 64;
+  for (int64_t tile = blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t c0 = tile * 64 + lane;
+    const bool valid = c0 < M.ncells;
+    const int64_t c = valid ? c0 : M.ncells - 1;  // lanes past the end fill the tile's padding
+    double* tb = rec + tile * (64 * R::SIZE);
+    double Ji[GD][GD];
+    const double det = fabs(simplex_geometry<GD>(M, c, Ji));
+#pragma unroll
+    for (int i = 0; i < GD; ++i)
+#pragma unroll
+      for (int k = 0; k < GD; ++k) sb[lane * QO + i * GD + k] = Ji[i][k];
+    sb[lane * QO + N] = det;
+#pragma unroll
+    for (int t = N + 1; t < QO; ++t) sb[lane * QO + t] = 0.0;
+    flush(tb, 64 * QO);
+    double lam, mu;
+    cell_lame(F, c, lam, mu);
+    const int32_t* cn = M.cells + c * NN;
+    for (int q = 0; q < NQ; ++q) {
+      double Fq[N];
+      deformation_gradient<GD>(F.u, cn, NN, tab + NQ + q * NN * GD, Ji, Fq);
+      double I1 = GD == 2 ? 1.0 : 0.0, J;
+#pragma unroll
+      for (int m = 0; m < N; ++m) I1 = fma(Fq[m], Fq[m], I1);
+      if constexpr (GD == 2) J = Fq[0] * Fq[3] - Fq[1] * Fq[2];
+      else J = Fq[0] * (Fq[4] * Fq[8] - Fq[5] * Fq[7]) - Fq[1] * (Fq[3] * Fq[8] - Fq[5] * Fq[6]) +
+               Fq[2] * (Fq[3] * Fq[7] - Fq[4] * Fq[6]);
+      double co[5];
+      neo_energy_coeffs(I1, J, lam, mu, co);
+      double Cm[GD][GD];
+      cofactor<GD>(Fq, Cm);
+#pragma unroll
+      for (int m = 0; m < N; ++m) sb[lane * QS + m] = Cm[m / GD][m % GD];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) sb[lane * QS + N + t] = co[2 + t];
+#pragma unroll
+      for (int t = N + 3; t < QS; ++t) sb[lane * QS + t] = 0.0;
+      flush(tb + 64 * QO + q * (64 * QS), 64 * QS);
+    }
+    if (bcmask && valid) {
+      uint32_t m = 0;
+#pragma unroll
+      for (int b = 0; b < NN; ++b) {
+        const int64_t n = cn[b];
+#pragma unroll
+        for (int j = 0; j < GD; ++j) m |= (bc[n * GD + j] ? 1u : 0u) << (b * GD + j);
+      }
+      bcmask[c] = m;
+    }
   }
 }
 
@@ -1866,7 +1961,7 @@ void k_gather(GatherArgs P) {
       mask = pmask;
     } else {
     if constexpr (MAT != MAT_BLOCKS && FA_ABL != 9) {
-      const double2* rp = reinterpret_cast<const double2*>(P.rec + c * R::SIZE);
+      const double2* rp = reinterpret_cast<const double2*>(P.rec + R::head(c));
 #pragma unroll
       for (int k = 0; k < RL / 2; ++k) {
         double2 v = rp[k];
@@ -1937,7 +2032,7 @@ void k_gather(GatherArgs P) {
         // invariant form (neo_energy_coeffs), 14 record values per point, the next point's values
         // loaded while this one is contracted: per column K_ab += c2 Ca Cb^T - c3 Cb Ca^T +
         // c4 (ga.gb) I [+ c0 Fa Fb^T + c1 (Fa Cb^T + Ca Fb^T)], Ca = cof(F) ga, Fa = F ga
-        const double* Q0 = P.rec + c * R::SIZE + R::QOFF;
+        const double* Q0 = P.rec + R::point0(c);
         constexpr int NL = FA_NEO_CREC ? N + 3 : N + 5;
         double Qn[NL];
 #pragma unroll
@@ -1948,7 +2043,7 @@ void k_gather(GatherArgs P) {
 #pragma unroll
           for (int t = 0; t < NL; ++t) Qc[t] = Qn[t];
           {
-            const double* Qx = Q0 + min(q + 1, NQ - 1) * R::QSTR;  // next point (the last one re-reads)
+            const double* Qx = Q0 + min(q + 1, NQ - 1) * R::PSTR;  // next point (the last one re-reads)
 #pragma unroll
             for (int t = 0; t < NL; ++t) Qn[t] = Qx[t];
           }
@@ -4165,7 +4260,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     if (MAT != FA_NEO_HOOKEAN && !(e && e[0] == '1')) P.corder = nullptr;
   }
   const int64_t nc = P.M.ncells;
-  const int64_t rec_bytes = align256((int64_t)sizeof(double) * R::SIZE * nc);
+  const int64_t rec_bytes = align256((int64_t)sizeof(double) * R::count(nc));
   if (W.mode == GatherStage::SIZE) {
     *W.bytes = rec_bytes + align256((int64_t)sizeof(uint32_t) * nc);
     return FA_OK;
@@ -4174,14 +4269,15 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   uint32_t* mask = nullptr;
   int rc;
   if (W.mode == GatherStage::FULL) {
-    if ((rc = scratch_alloc((void**)&rec, sizeof(double) * R::SIZE * nc, s))) return rc;
+    if ((rc = scratch_alloc((void**)&rec, sizeof(double) * R::count(nc), s))) return rc;
     if (bc && (rc = scratch_alloc((void**)&mask, sizeof(uint32_t) * nc, s))) return rc;
   } else {
     rec = reinterpret_cast<double*>(W.work);
     mask = bc ? reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.work) + rec_bytes) : nullptr;
   }
   if (nc > 0 && W.mode != GatherStage::ROWS) {
-    k_cell_records<GD, NN, NV, NQ, MAT><<<grid_for(nc), 256, 0, s>>>(P.M, P.F, P.tab, bc, rec, mask);
+    if constexpr (R::TILED) k_neo_records_tiled<GD, NN, NV, NQ><<<grid_for(nc), 256, 0, s>>>(P.M, P.F, P.tab, bc, rec, mask);
+    else k_cell_records<GD, NN, NV, NQ, MAT><<<grid_for(nc), 256, 0, s>>>(P.M, P.F, P.tab, bc, rec, mask);
     LAUNCH_CHECK();
   }
   P.rec = rec;
