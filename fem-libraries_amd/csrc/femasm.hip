@@ -1002,6 +1002,9 @@ constexpr int MAT_AFFT = 11;
 #ifndef FA_NEO_TILE
 #define FA_NEO_TILE 1  // neo-Hookean C records in 64-cell tiles (Rec::TILED)
 #endif
+#ifndef FA_REC_STAGED
+#define FA_REC_STAGED 1  // small records stored through LDS as contiguous runs (k_cell_records_staged)
+#endif
 template <int GD, int NV, int NQ, int MAT>
 struct Rec {
   static constexpr bool SIMP = (NV == GD + 1) || MAT == MAT_AFFT;  // affine: one Jacobian per cell
@@ -1075,6 +1078,95 @@ struct GatherArgs {
   const uint16_t* cwords;  // per chunk: 256 lane starts, then K x 256 contribution words
 };
 
+// The record of cell c for the gather (all kinds but the neo-Hookean tangents): see Rec.
+template <int GD, int NN, int NV, int NQ, int MAT>
+__device__ __forceinline__ void cell_record(const MeshView& M, const FormView& F, const double* __restrict__ tab, int64_t c,
+                                            double (&r)[Rec<GD, NV, NQ, MAT>::SIZE]) {
+  using R = Rec<GD, NV, NQ, MAT>;
+#pragma unroll
+  for (int k = 0; k < R::SIZE; ++k) r[k] = 0.0;
+  if constexpr (MAT == FA_ASYM_DAMAGE) {
+    double g[3][2], w, H[3][3];
+    damage_cell(M, F, c, g, w, H);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { r[2 * a] = g[a][0]; r[2 * a + 1] = g[a][1]; }
+    r[6] = w;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) r[7 + 3 * i + j] = H[i][j];
+  } else if constexpr (MAT == MAT_LINU || MAT == MAT_AFFT) {
+    static_assert(R::SIMP, "uniform-nu records: affine cells");
+    double lam, mu;
+    cell_lame(F, c, lam, mu);
+    double Ji[GD][GD];
+    const double s2 = mu * fabs(MAT == MAT_AFFT ? affine_tensor_geometry<GD, NV>(M, c, Ji) : simplex_geometry<GD>(M, c, Ji));
+    const double sc = sqrt(fabs(s2));
+#pragma unroll
+    for (int i = 0; i < GD; ++i)
+#pragma unroll
+      for (int k = 0; k < GD; ++k) r[i * GD + k] = sc * Ji[i][k];
+    r[GD * GD] = s2 < 0.0 ? -1.0 : 1.0;
+  } else {
+    double lam, mu;
+    cell_lame(F, c, lam, mu);
+    if constexpr (R::SIMP) {
+      double Ji[GD][GD];
+      double det = simplex_geometry<GD>(M, c, Ji);
+#pragma unroll
+      for (int i = 0; i < GD; ++i)
+#pragma unroll
+        for (int k = 0; k < GD; ++k) r[i * GD + k] = Ji[i][k];
+      r[GD * GD] = fabs(det);
+      r[GD * GD + 1] = lam;
+      r[GD * GD + 2] = mu;
+    } else {
+      double xv[NV][GD];
+      const int32_t* gv = M.geom + c * NV;
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int i = 0; i < GD; ++i) xv[v][i] = M.x[(int64_t)gv[v] * GD + i];
+      const double* gdphi = tab + NQ + NQ * NN * GD;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        double Ji[GD][GD];
+        double det = tensor_geometry<GD, NV>(xv, gdphi + q * NV * GD, Ji);
+#pragma unroll
+        for (int i = 0; i < GD; ++i)
+#pragma unroll
+          for (int k = 0; k < GD; ++k) r[q * (GD * GD + 1) + i * GD + k] = Ji[i][k];
+        r[q * (GD * GD + 1) + GD * GD] = fabs(det);
+      }
+      r[NQ * (GD * GD + 1)] = lam;
+      r[NQ * (GD * GD + 1) + 1] = mu;
+    }
+  }
+}
+
+// constrained-dof bits of cell c (bit b*GD+j), or "touches a constrained dof" for cells with more
+// dofs than mask bits (the gather looks those up)
+template <int GD, int NN>
+__device__ __forceinline__ uint32_t cell_bcmask(const MeshView& M, const int8_t* __restrict__ bc, int64_t c) {
+  uint32_t m = 0;
+  const int32_t* cn = M.cells + c * NN;
+  if constexpr (NN * GD <= 32) {
+#pragma unroll
+    for (int b = 0; b < NN; ++b) {
+      int64_t n = cn[b];
+#pragma unroll
+      for (int j = 0; j < GD; ++j) m |= (bc[n * GD + j] ? 1u : 0u) << (b * GD + j);
+    }
+  } else {
+    for (int b = 0; b < NN; ++b) {
+      int64_t n = cn[b];
+#pragma unroll
+      for (int j = 0; j < GD; ++j) m |= bc[n * GD + j] ? 1u : 0u;
+    }
+  }
+  return m;
+}
+
 template <int GD, int NN, int NV, int NQ, int MAT>
 __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, const double* __restrict__ tab,
                                                       const int8_t* __restrict__ bc, double* __restrict__ rec,
@@ -1144,88 +1236,47 @@ __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, co
     }
   } else {
   double r[R::SIZE];
-#pragma unroll
-  for (int k = 0; k < R::SIZE; ++k) r[k] = 0.0;
-  if constexpr (MAT == FA_ASYM_DAMAGE) {
-    double g[3][2], w, H[3][3];
-    damage_cell(M, F, c, g, w, H);
-#pragma unroll
-    for (int a = 0; a < 3; ++a) { r[2 * a] = g[a][0]; r[2 * a + 1] = g[a][1]; }
-    r[6] = w;
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) r[7 + 3 * i + j] = H[i][j];
-  } else if constexpr (MAT == MAT_LINU || MAT == MAT_AFFT) {
-    static_assert(R::SIMP, "uniform-nu records: affine cells");
-    double lam, mu;
-    cell_lame(F, c, lam, mu);
-    double Ji[GD][GD];
-    const double s2 = mu * fabs(MAT == MAT_AFFT ? affine_tensor_geometry<GD, NV>(M, c, Ji) : simplex_geometry<GD>(M, c, Ji));
-    const double sc = sqrt(fabs(s2));
-#pragma unroll
-    for (int i = 0; i < GD; ++i)
-#pragma unroll
-      for (int k = 0; k < GD; ++k) r[i * GD + k] = sc * Ji[i][k];
-    r[GD * GD] = s2 < 0.0 ? -1.0 : 1.0;
-  } else {
-    double lam, mu;
-    cell_lame(F, c, lam, mu);
-    if constexpr (R::SIMP) {
-      double Ji[GD][GD];
-      double det = simplex_geometry<GD>(M, c, Ji);
-#pragma unroll
-      for (int i = 0; i < GD; ++i)
-#pragma unroll
-        for (int k = 0; k < GD; ++k) r[i * GD + k] = Ji[i][k];
-      r[GD * GD] = fabs(det);
-      r[GD * GD + 1] = lam;
-      r[GD * GD + 2] = mu;
-    } else {
-      double xv[NV][GD];
-      const int32_t* gv = M.geom + c * NV;
-#pragma unroll
-      for (int v = 0; v < NV; ++v)
-#pragma unroll
-        for (int i = 0; i < GD; ++i) xv[v][i] = M.x[(int64_t)gv[v] * GD + i];
-      const double* gdphi = tab + NQ + NQ * NN * GD;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        double Ji[GD][GD];
-        double det = tensor_geometry<GD, NV>(xv, gdphi + q * NV * GD, Ji);
-#pragma unroll
-        for (int i = 0; i < GD; ++i)
-#pragma unroll
-          for (int k = 0; k < GD; ++k) r[q * (GD * GD + 1) + i * GD + k] = Ji[i][k];
-        r[q * (GD * GD + 1) + GD * GD] = fabs(det);
-      }
-      r[NQ * (GD * GD + 1)] = lam;
-      r[NQ * (GD * GD + 1) + 1] = mu;
-    }
-  }
+  cell_record<GD, NN, NV, NQ, MAT>(M, F, tab, c, r);
   double2* out = reinterpret_cast<double2*>(rec + c * R::SIZE);
 #pragma unroll
   for (int k = 0; k < R::SIZE / 2; ++k) out[k] = make_double2(r[2 * k], r[2 * k + 1]);
   }
-  if (bcmask) {
-    uint32_t m = 0;
-    const int32_t* cn = M.cells + c * NN;
-    if constexpr (NN * GD <= 32) {
-#pragma unroll
-      for (int b = 0; b < NN; ++b) {
-        int64_t n = cn[b];
-#pragma unroll
-        for (int j = 0; j < GD; ++j) m |= (bc[n * GD + j] ? 1u : 0u) << (b * GD + j);
-      }
-    } else {  // too many dofs for a bit mask: "the cell touches a constrained dof" (the gather looks them up)
-      for (int b = 0; b < NN; ++b) {
-        int64_t n = cn[b];
-#pragma unroll
-        for (int j = 0; j < GD; ++j) m |= bc[n * GD + j] ? 1u : 0u;
-      }
-    }
-    bcmask[c] = m;
+  if (bcmask) bcmask[c] = cell_bcmask<GD, NN>(M, bc, c);
   }
+}
+
+// Records of at most 16 doubles (uniform-nu and general linear simplices, affine tensor cells, the
+// damage law): a wave's 64 consecutive cells' records are one contiguous run; the lanes write them
+// into wave-private LDS and the wave stores the run with 16 B per lane (a lane storing its own
+// 80-B record touches one cache line per lane per store instruction). Config E: see DESIGN.md.
+template <int GD, int NN, int NV, int NQ, int MAT>
+__global__ __launch_bounds__(256) void k_cell_records_staged(MeshView M, FormView F, const double* __restrict__ tab,
+                                                             const int8_t* __restrict__ bc, double* __restrict__ rec,
+                                                             uint32_t* __restrict__ bcmask) {
+  using R = Rec<GD, NV, NQ, MAT>;
+  static_assert(R::SIZE <= 16 && MAT != FA_NEO_HOOKEAN, "staged records: small records");
+  __shared__ __attribute__((aligned(16))) double sbuf[4][64 * R::SIZE];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* sb = sbuf[wave];
+  for (int64_t cb = (int64_t)blockIdx.x * 256 + wave * 64; cb < M.ncells; cb += (int64_t)gridDim.x * 256) {
+    const int64_t c = cb + lane;
+    const bool valid = c < M.ncells;
+    const int64_t cc = valid ? c : M.ncells - 1;
+    double r[R::SIZE];
+    cell_record<GD, NN, NV, NQ, MAT>(M, F, tab, cc, r);
+#pragma unroll
+    for (int k = 0; k < R::SIZE; ++k) sb[lane * R::SIZE + k] = r[k];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int nv = (int)min<int64_t>(64, M.ncells - cb) * R::SIZE;  // even
+    const double2* s2 = reinterpret_cast<const double2*>(sb);
+    double2* d2 = reinterpret_cast<double2*>(rec + cb * R::SIZE);
+    for (int t = lane; t < nv / 2; t += 64) d2[t] = s2[t];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (bcmask && valid) bcmask[c] = cell_bcmask<GD, NN>(M, bc, c);
   }
 }
 
@@ -4277,6 +4328,8 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   }
   if (nc > 0 && W.mode != GatherStage::ROWS) {
     if constexpr (R::TILED) k_neo_records_tiled<GD, NN, NV, NQ><<<grid_for(nc), 256, 0, s>>>(P.M, P.F, P.tab, bc, rec, mask);
+    else if constexpr (R::SIZE <= 16 && MAT != FA_NEO_HOOKEAN && FA_REC_STAGED)
+      k_cell_records_staged<GD, NN, NV, NQ, MAT><<<grid_for(nc), 256, 0, s>>>(P.M, P.F, P.tab, bc, rec, mask);
     else k_cell_records<GD, NN, NV, NQ, MAT><<<grid_for(nc), 256, 0, s>>>(P.M, P.F, P.tab, bc, rec, mask);
     LAUNCH_CHECK();
   }
