@@ -730,18 +730,24 @@ __global__ void k_zero_window(BsrView A, int bs2) {
 // Ae and MODE 1 adds into the global BSR with FP64 atomics (dolfinx ADD_VALUES semantics).
 typedef double fa_d4 __attribute__((ext_vector_type(4)));
 
+// tiles per wave of k_hex_mfma: Q3 (16 tiles) runs 8 waves of 2 tiles, whose 18 accumulators fit
+// the 256 VGPRs of 2 waves / SIMD (16 waves of one tile were capped at 128 VGPRs and spilled 35)
+__host__ __device__ constexpr int hex_tpw(int nn) { return ((nn + 15) / 16) * ((nn + 15) / 16) >= 16 ? 2 : 1; }
+__host__ __device__ constexpr int hex_threads(int nn) { return 64 * ((nn + 15) / 16) * ((nn + 15) / 16) / hex_tpw(nn); }
+
 template <int NN, int NQ, int MODE>
-__global__ __launch_bounds__(64 * ((NN + 15) / 16) * ((NN + 15) / 16)) void k_hex_mfma(
+__global__ __launch_bounds__(hex_threads(NN)) void k_hex_mfma(
     MeshView M, FormView F, DevTables T, int64_t c0, int64_t ncells, double* __restrict__ Ae, BsrView A,
     const int8_t* __restrict__ bc, int* __restrict__ err) {
-  constexpr int NT = (NN + 15) / 16;  // 16-row tiles per side; one wave per (a, b) tile
-  constexpr int NTHR = 64 * NT * NT;
+  constexpr int NT = (NN + 15) / 16;  // 16-row tiles per side; TPW (a, b) tiles per wave
+  constexpr int TPW = hex_tpw(NN), NWAVE = NT * NT / TPW;
+  constexpr int NTHR = hex_threads(NN);
   constexpr int NNP = NT * 16 + 16;   // row stride: +16 doubles puts q and q+1 on opposite bank halves
   constexpr int QMAX = (NQ + 3) & ~3;
   __shared__ double phi[3][QMAX][NNP];
   __shared__ double sJ[QMAX][10];  // Ji (9) + sqrt(w |J|)
   __shared__ uint8_t s_bcn[NN];    // MODE 2: constrained-dof bits of the cell's nodes
-  static_assert(MODE != 2 || 3 * QMAX * NNP >= NT * NT * 64 * 9, "block staging fits the phi image");
+  static_assert(MODE != 2 || 3 * QMAX * NNP >= NWAVE * 64 * 9, "block staging fits the phi image");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nq = NQ, nqp = QMAX;
   for (int64_t ci = blockIdx.x; ci < ncells; ci += gridDim.x) {
@@ -788,31 +794,44 @@ __global__ __launch_bounds__(64 * ((NN + 15) / 16) * ((NN + 15) / 16)) void k_he
     double lam, mu;
     cell_lame(F, c, lam, mu);
     const int32_t* cn = M.cells + c * NN;
-    for (int t = wave; t < NT * NT; t += NT * NT) {
-      const int ta = t / NT, tb = t % NT;
-      fa_d4 acc[9];
+    fa_d4 accs[TPW][9];
 #pragma unroll
-      for (int m = 0; m < 9; ++m) acc[m] = fa_d4{0.0, 0.0, 0.0, 0.0};
-      const int ra = ta * 16 + (lane & 15), rb = tb * 16 + (lane & 15), kq = lane >> 4;
+    for (int j = 0; j < TPW; ++j)
+#pragma unroll
+      for (int m = 0; m < 9; ++m) accs[j][m] = fa_d4{0.0, 0.0, 0.0, 0.0};
+    {
+      const int kq = lane >> 4;
       for (int q0 = 0; q0 < nqp; q0 += 4) {
-        double av[3], bv[3];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          av[i] = phi[i][q0 + kq][ra];  // A[a][q] = Phi_i
-          bv[i] = phi[i][q0 + kq][rb];  // B[q][b] = Phi_k^T
+        for (int j = 0; j < TPW; ++j) {
+          const int t = wave + j * NWAVE, ta = t / NT, tb = t % NT;
+          const int ra = ta * 16 + (lane & 15), rb = tb * 16 + (lane & 15);
+          double av[3], bv[3];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            av[i] = phi[i][q0 + kq][ra];  // A[a][q] = Phi_i
+            bv[i] = phi[i][q0 + kq][rb];  // B[q][b] = Phi_k^T
+          }
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+              accs[j][i * 3 + k] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[k], accs[j][i * 3 + k], 0, 0, 0);
         }
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int k = 0; k < 3; ++k) acc[i * 3 + k] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[k], acc[i * 3 + k], 0, 0, 0);
       }
+    }
+    if constexpr (MODE == 2) __syncthreads();  // every wave is past its MFMA loop: phi is free
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      const int t = wave + j * NWAVE;
+      const int ta = t / NT, tb = t % NT;
+      const fa_d4 (&acc)[9] = accs[j];
       // D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * r
       if constexpr (MODE == 2) {
         // block store for the row gather, Eb[c][a][b][3][3] with bc rows / columns zeroed: the
         // wave's 4 x 16 blocks of each r go through a wave-private slice of the (now unused) phi
         // image and leave as contiguous 8-B-per-lane stores (512 B per instruction), instead of
         // nine 72-B-strided stores per lane
-        __syncthreads();  // every wave is past its MFMA loop: phi is free
         double* st = &phi[0][0][0] + wave * (64 * 9);
         const int nbv = min(16, NN - tb * 16);  // valid column blocks of this tile
 #pragma unroll
@@ -903,7 +922,7 @@ static int launch_hex_mfma(int mode, const fa_mesh* mesh, const MeshView& M, con
   const int grid = (int)std::min<int64_t>(nc, kMaxBlocks);
 #define HEXL(NN, NQ)                                                                                          \
   do {                                                                                                        \
-    constexpr int thr = 64 * ((NN + 15) / 16) * ((NN + 15) / 16);                                             \
+    constexpr int thr = hex_threads(NN);                                                                      \
     if (mode == 0) k_hex_mfma<NN, NQ, 0><<<grid, thr, 0, s>>>(M, F, T, c0, nc, Ae, A, bc, derr);               \
     else if (mode == 2) k_hex_mfma<NN, NQ, 2><<<grid, thr, 0, s>>>(M, F, T, c0, nc, Ae, A, bc, derr);          \
     else k_hex_mfma<NN, NQ, 1><<<grid, thr, 0, s>>>(M, F, T, c0, nc, Ae, A, bc, derr);                        \
@@ -4445,7 +4464,7 @@ static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc,
     eb = reinterpret_cast<double*>(W.work);
   }
   if (nc > 0 && W.mode != GatherStage::ROWS) {
-    constexpr int thr = 64 * ((NN + 15) / 16) * ((NN + 15) / 16);
+    constexpr int thr = hex_threads(NN);
     const int grid = (int)std::min<int64_t>(nc, kMaxBlocks);
     BsrView none{nullptr, nullptr, nullptr, 0, 0};
     k_hex_mfma<NN, NQ, 2><<<grid, thr, 0, s>>>(P.M, P.F, T, 0, nc, eb, none, bc, P.err);
