@@ -510,11 +510,15 @@ def _plan_locality(V, fm, adj, plan, sh):
 
 def _use_contrib(V, kind) -> bool:
     """Block-owner gather (fa_plan_contrib) for linear elasticity on P1/P2 triangles and
-    tetrahedra, opt-in with FEMASM_CONTRIB=1 (measured slower than the LDS-atomic gather on
-    configs C and E)."""
-    if os.environ.get("FEMASM_CONTRIB", "0") != "1" or kind != _lib.FA_LINEAR_ELASTICITY:
+    tetrahedra. FEMASM_CONTRIB: "auto" (default) uses it for triangles, where it measured faster
+    (config A 0.136 vs 0.220 ms), and keeps the LDS-atomic gather for tetrahedra, where that one
+    is faster (C 1.72 vs 2.07 ms, E 46.8 vs 53.1 ms); "1" / "0" force it."""
+    mode = os.environ.get("FEMASM_CONTRIB", "auto")
+    if mode == "0" or kind != _lib.FA_LINEAR_ELASTICITY or V.degree not in (1, 2):
         return False
-    return V.mesh.cell_type in (_lib.FA_TRIANGLE, _lib.FA_TETRAHEDRON) and V.degree in (1, 2)
+    if mode == "1":
+        return V.mesh.cell_type in (_lib.FA_TRIANGLE, _lib.FA_TETRAHEDRON)
+    return V.mesh.cell_type == _lib.FA_TRIANGLE
 
 
 def _plan_contrib(V, fm, adj, fb, rs, plan, sh):
