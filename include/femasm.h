@@ -188,7 +188,7 @@ int fa_plan_locality(const fa_mesh* mesh, const fa_adjacency* adj, int32_t* cord
 
 /* Block-owner gather (P1/P2 triangles and tetrahedra, linear elasticity with one Poisson ratio).
  * fa_plan_gather_contrib chunks the rows for it (like fa_plan_gather, smaller chunks: at most
- * 128 adjacency entries). fa_plan_contrib_bytes returns the device buffer size the contribution
+ * 256 adjacency entries). fa_plan_contrib_bytes returns the device buffer size the contribution
  * plan of that chunking needs; fa_plan_contrib fills a caller-owned buffer of that size with
  * every chunk's (cell, row node, column node) contributions sorted by destination block and cut
  * into equal lane segments, and sets plan->contrib. The assembly then sums each block's
