@@ -67,6 +67,7 @@ def test_in_kernel_slot_search(dev, oracle, monkeypatch, ct, p, n):
     from femasm import fem
 
     monkeypatch.setenv("FEMASM_SLOTS", "0")
+    monkeypatch.setenv("FEMASM_CONTRIB", "0")  # the LDS-atomic gather's plan (triangles default to the owner plan)
     V, a, bcs, indptr, indices, ref = _problem(dev, oracle, ct, p, n)
     A = fem.assemble_matrix(a, bcs=bcs)
     plan_entry = next(iter(V.__dict__["_plans"].values()))
@@ -85,6 +86,7 @@ def test_slot_order(dev, oracle, monkeypatch, order, ct, p, n):
     from femasm import fem
 
     monkeypatch.setenv("FEMASM_SLOT_ORDER", order)
+    monkeypatch.setenv("FEMASM_CONTRIB", "0")  # the LDS-atomic gather's plan refinements
     V, a, bcs, indptr, indices, ref = _problem(dev, oracle, ct, p, n)
     A = fem.assemble_matrix(a, bcs=bcs)
     plan = next(iter(V.__dict__["_plans"].values()))[0]
@@ -103,6 +105,7 @@ def test_chunk_locality_order(dev, oracle, monkeypatch, order, ct, p, n):
     from femasm import fem
 
     monkeypatch.setenv("FEMASM_CHUNK_ORDER", order)
+    monkeypatch.setenv("FEMASM_CONTRIB", "0")  # the LDS-atomic gather's plan refinements
     V, a, bcs, indptr, indices, ref = _problem(dev, oracle, ct, p, n)
     A = fem.assemble_matrix(a, bcs=bcs)
     entry = next(iter(V.__dict__["_plans"].values()))
