@@ -1021,6 +1021,13 @@ constexpr int MAT_AFFT = 11;
 #ifndef FA_NEO_TILE
 #define FA_NEO_TILE 1  // neo-Hookean C records in 64-cell tiles (Rec::TILED)
 #endif
+#ifndef FA_NEO_SREC
+// tiled C records with the cofactor scaled: W_JJ + W_J/J = lam / J^2 has the sign s_c of the cell's
+// lam at every point and 2 W_1 = mu is constant, so a point needs only C' = sqrt|c2| C and
+// rho = c3 / |c2| (10 doubles instead of 12), the head s_c and mu: K_ab += s_c C'ga (C'gb)^T -
+// rho C'gb (C'ga)^T + mu (ga.gb) I (lam = 0: C' = C, s_c = 0, rho = c3)
+#define FA_NEO_SREC 1
+#endif
 #ifndef FA_REC_STAGED
 #define FA_REC_STAGED 1  // small records stored through LDS as contiguous runs (k_cell_records_staged)
 #endif
@@ -1034,8 +1041,10 @@ struct Rec {
   // NEO per quadrature point (FA_NEO_INV): F[GD*GD] and the strain-energy coefficients s11, s1J,
   // sCC, sCt, s1 (neo_energy_coeffs) from QOFF, stride QSTR; FA_NEO_INV=0: the 45-entry upper
   // triangle of dP/dF at N + 1, stride NTRI
-  static constexpr int QOFF = FA_NEO_INV ? ((N + 2) & ~1) : N + 1;
-  static constexpr int QSTR = FA_NEO_INV ? (FA_NEO_CREC ? ((N + 4) & ~1) : ((N + 6) & ~1)) : NTRI;
+  static constexpr bool SREC = MAT == FA_NEO_HOOKEAN && FA_NEO_INV && FA_NEO_CREC && FA_NEO_TILE && FA_NEO_SREC;
+  // SREC head: J^-1, |J|, s_c, mu | point: C' (N), rho
+  static constexpr int QOFF = SREC ? ((N + 4) & ~1) : (FA_NEO_INV ? ((N + 2) & ~1) : N + 1);
+  static constexpr int QSTR = SREC ? ((N + 2) & ~1) : (FA_NEO_INV ? (FA_NEO_CREC ? ((N + 4) & ~1) : ((N + 6) & ~1)) : NTRI);
   static constexpr int RAW = MAT == MAT_BLOCKS ? 2
                              : (MAT == MAT_LINU || MAT == MAT_AFFT) ? GD * GD + 1
                              : MAT == FA_ASYM_DAMAGE ? 16
@@ -1334,6 +1343,9 @@ __global__ __launch_bounds__(256) void k_neo_records_tiled(MeshView M, FormView 
     double* tb = rec + tile * (64 * R::SIZE);
     double Ji[GD][GD];
     const double det = fabs(simplex_geometry<GD>(M, c, Ji));
+    double lam, mu;
+    cell_lame(F, c, lam, mu);
+    const double sgn = lam > 0.0 ? 1.0 : (lam < 0.0 ? -1.0 : 0.0);  // sign of W_JJ + W_J/J = lam / J^2
 #pragma unroll
     for (int i = 0; i < GD; ++i)
 #pragma unroll
@@ -1341,9 +1353,11 @@ __global__ __launch_bounds__(256) void k_neo_records_tiled(MeshView M, FormView 
     sb[lane * QO + N] = det;
 #pragma unroll
     for (int t = N + 1; t < QO; ++t) sb[lane * QO + t] = 0.0;
+    if constexpr (R::SREC) {
+      sb[lane * QO + N + 1] = sgn;
+      sb[lane * QO + N + 2] = mu;  // 2 W_1 of neo_energy (W is mu/2 I1 + terms in J)
+    }
     flush(tb, 64 * QO);
-    double lam, mu;
-    cell_lame(F, c, lam, mu);
     const int32_t* cn = M.cells + c * NN;
     for (int q = 0; q < NQ; ++q) {
       double Fq[N];
@@ -1358,12 +1372,23 @@ __global__ __launch_bounds__(256) void k_neo_records_tiled(MeshView M, FormView 
       neo_energy_coeffs(I1, J, lam, mu, co);
       double Cm[GD][GD];
       cofactor<GD>(Fq, Cm);
+      if constexpr (R::SREC) {
+        const double a2 = fabs(co[2]);
+        const double sc = sgn != 0.0 ? sqrt(a2) : 1.0;
+        const double rho = sgn != 0.0 ? co[3] / a2 : co[3];
 #pragma unroll
-      for (int m = 0; m < N; ++m) sb[lane * QS + m] = Cm[m / GD][m % GD];
+        for (int m = 0; m < N; ++m) sb[lane * QS + m] = sc * Cm[m / GD][m % GD];
+        sb[lane * QS + N] = rho;
 #pragma unroll
-      for (int t = 0; t < 3; ++t) sb[lane * QS + N + t] = co[2 + t];
+        for (int t = N + 1; t < QS; ++t) sb[lane * QS + t] = 0.0;
+      } else {
 #pragma unroll
-      for (int t = N + 3; t < QS; ++t) sb[lane * QS + t] = 0.0;
+        for (int m = 0; m < N; ++m) sb[lane * QS + m] = Cm[m / GD][m % GD];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) sb[lane * QS + N + t] = co[2 + t];
+#pragma unroll
+        for (int t = N + 3; t < QS; ++t) sb[lane * QS + t] = 0.0;
+      }
       flush(tb + 64 * QO + q * (64 * QS), 64 * QS);
     }
     if (bcmask && valid) {
@@ -2009,7 +2034,7 @@ void k_gather(GatherArgs P) {
     const int lo = posm ? 0 : rowoff[lr], hi = posm ? 0 : rowoff[lr + 1];
     // one record + the column nodes + the bc mask: all independent loads, issued together
     // registers: NEO keeps only Ji, wdet; tensor cells read their per-q records in the q loop
-    constexpr int RL = NEO ? ((BS2 + 2) & ~1) : (SIMP || MAT == FA_ASYM_DAMAGE ? R::SIZE : 2);
+    constexpr int RL = NEO ? (R::SREC ? R::QOFF : ((BS2 + 2) & ~1)) : (SIMP || MAT == FA_ASYM_DAMAGE ? R::SIZE : 2);
     double r[RL];
 #if FA_ABL == 7 || FA_ABL == 9
 #pragma unroll
@@ -2103,7 +2128,7 @@ void k_gather(GatherArgs P) {
         // loaded while this one is contracted: per column K_ab += c2 Ca Cb^T - c3 Cb Ca^T +
         // c4 (ga.gb) I [+ c0 Fa Fb^T + c1 (Fa Cb^T + Ca Fb^T)], Ca = cof(F) ga, Fa = F ga
         const double* Q0 = P.rec + R::point0(c);
-        constexpr int NL = FA_NEO_CREC ? N + 3 : N + 5;
+        constexpr int NL = R::SREC ? N + 1 : (FA_NEO_CREC ? N + 3 : N + 5);
         double Qn[NL];
 #pragma unroll
         for (int t = 0; t < NL; ++t) Qn[t] = Q0[t];
@@ -2136,8 +2161,10 @@ void k_gather(GatherArgs P) {
             cofactor<GD>(Fq, Cm);
           }
           constexpr int CO = FA_NEO_CREC ? N - 2 : N;  // index of c0 (c0, c1 absent from C records)
-          const double c0 = FA_NEO_CREC ? 0.0 : Qc[CO], c1 = FA_NEO_CREC ? 0.0 : Qc[CO + 1], c2 = Qc[CO + 2],
-                       c3 = Qc[CO + 3], c4 = Qc[CO + 4];
+          // SREC: C' = sqrt|c2| C in the record, c2 -> the head's sign, c3 -> rho, c4 -> the head's mu
+          const double c0 = FA_NEO_CREC ? 0.0 : Qc[min(CO, NL - 1)], c1 = FA_NEO_CREC ? 0.0 : Qc[min(CO + 1, NL - 1)],
+                       c2 = R::SREC ? r[N + 1] : Qc[min(CO + 2, NL - 1)], c3 = R::SREC ? Qc[N] : Qc[min(CO + 3, NL - 1)],
+                       c4 = R::SREC ? r[N + 2] : Qc[min(CO + 4, NL - 1)];
           double u[GD], v[GD];
 #pragma unroll
           for (int i = 0; i < GD; ++i) {
