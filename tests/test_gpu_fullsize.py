@@ -18,11 +18,16 @@ def dev():
     return torch.device("cuda", 0)
 
 
+@pytest.mark.parametrize("contrib", ["0", "1"], ids=["lds-atomic", "block-owner"])
 @pytest.mark.parametrize("n", [203])
-def test_config_e_p2_tet_full_size(oracle, dev, n):
-    """Config E mesh (203^3 x 6 = 50.2 M P2 tets, 202 M dofs) with the reference bcs."""
+def test_config_e_p2_tet_full_size(oracle, dev, monkeypatch, n, contrib):
+    """Config E mesh (203^3 x 6 = 50.2 M P2 tets, 202 M dofs) with the reference bcs, through the
+    default LDS-atomic gather and through the block-owner gather (FEMASM_CONTRIB=1: ~4.9 M chunks
+    of the contribution plan at full size)."""
     from femasm import fem, mesh
     from femasm.materials import e_range
+
+    monkeypatch.setenv("FEMASM_CONTRIB", contrib)
 
     m = mesh.create_unit_cube(n, n, n, mesh.CellType.tetrahedron, device=dev)
     V = fem.functionspace(m, ("Lagrange", 2, (3,)))
