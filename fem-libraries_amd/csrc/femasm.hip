@@ -5134,3 +5134,127 @@ extern "C" int fa_bsr_block_diag(const fa_bsr* A, double* out, void* stream) {
   LAUNCH_CHECK();
   return FA_OK;
 }
+
+// ------------------------------------------------------------------------------------ HBM probe
+// Measured HBM peak beside the 8 TB/s spec: a grid-stride stream over n doubles with
+// 16 B per lane and four independent accesses in flight per lane. mode 0: copy src -> dst (read +
+// write), 1: write only (dst = v), 2: read only (src summed into one double per workgroup, dst[block]).
+template <int MODE, int ST = 0>
+__global__ __launch_bounds__(256) void k_hbm_probe(double* __restrict__ dst, const double* __restrict__ src, int64_t n2,
+                                                   double v) {
+  typedef double dv2 __attribute__((ext_vector_type(2)));
+  dv2* d2 = reinterpret_cast<dv2*>(dst);
+  const dv2* s2 = reinterpret_cast<const dv2*>(src);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  double sum = 0.0;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n2; t += 4 * stride) {
+    dv2 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = t + u * stride;
+      if (MODE != 1 && i < n2) x[u] = __builtin_nontemporal_load(s2 + i);
+      else x[u] = dv2{v, v};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = t + u * stride;
+      if (i < n2) {
+        if (MODE == 2) sum += x[u].x + x[u].y;
+        else if (ST == 0) __builtin_nontemporal_store(x[u], d2 + i);
+        else d2[i] = x[u];
+      }
+    }
+  }
+  if (MODE == 2) {
+    __shared__ double red[256];
+    red[threadIdx.x] = sum;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+      if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) dst[blockIdx.x] = red[0];
+  }
+}
+
+// write-pattern variants (measurement): each wave writes SPAN consecutive KiB per round (16 B per
+// lane per instruction), rounds grid-strided; LANE64: each lane writes 64 contiguous bytes instead
+template <int SPAN, bool NT, bool LANE64>
+__global__ __launch_bounds__(256) void k_hbm_write_span(double* __restrict__ dst, int64_t n2, double v) {
+  typedef double dv2 __attribute__((ext_vector_type(2)));
+  dv2* d2 = reinterpret_cast<dv2*>(dst);
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t per = 64 * SPAN;  // dv2 per wave round
+  const dv2 x = dv2{v, v};
+  for (int64_t base = wave * per; base < n2; base += nwaves * per) {
+#pragma unroll
+    for (int u = 0; u < SPAN; ++u) {
+      const int64_t i = LANE64 ? base + (int64_t)lane * SPAN + u : base + u * 64 + lane;
+      if (i < n2) {
+        if (NT) __builtin_nontemporal_store(x, d2 + i);
+        else d2[i] = x;
+      }
+    }
+  }
+}
+
+extern "C" int fa_hbm_probe(int32_t mode, double* dst, const double* src, int64_t n, void* stream) {
+  if (n <= 0 || (n & 1)) return fail(FA_E_ARG, "n must be positive and even");
+  if (!dst || (mode != 1 && !src)) return fail(FA_E_ARG, "null argument");
+  if (((uintptr_t)dst | (uintptr_t)src) & 15) return fail(FA_E_ARG, "buffers must be 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int grid = cus * 8;  // mode 2 writes one double per workgroup: dst holds >= grid doubles
+  if (mode == 2 && n < grid) return fail(FA_E_ARG, "read probe needs n >= %d", grid);
+  switch (mode) {
+    case 0: k_hbm_probe<0><<<grid, 256, 0, s>>>(dst, src, n / 2, 0.0); break;
+    case 1: k_hbm_probe<1><<<grid, 256, 0, s>>>(dst, src, n / 2, 1.0); break;
+    case 2: k_hbm_probe<2><<<grid, 256, 0, s>>>(dst, src, n / 2, 0.0); break;
+    // store-flavour variants of the write / copy streams (measurement): plain stores, larger grids
+    case 3: k_hbm_probe<1, 1><<<grid, 256, 0, s>>>(dst, src, n / 2, 1.0); break;
+    case 5: k_hbm_probe<0, 1><<<grid, 256, 0, s>>>(dst, src, n / 2, 0.0); break;
+    case 6: k_hbm_probe<1, 0><<<grid * 4, 256, 0, s>>>(dst, src, n / 2, 1.0); break;
+    case 7: k_hbm_probe<1, 1><<<grid * 4, 256, 0, s>>>(dst, src, n / 2, 1.0); break;
+    case 10: k_hbm_write_span<4, true, false><<<grid, 256, 0, s>>>(dst, n / 2, 1.0); break;
+    case 11: k_hbm_write_span<4, false, false><<<grid, 256, 0, s>>>(dst, n / 2, 1.0); break;
+    case 12: k_hbm_write_span<16, true, false><<<grid, 256, 0, s>>>(dst, n / 2, 1.0); break;
+    case 13: k_hbm_write_span<16, false, false><<<grid, 256, 0, s>>>(dst, n / 2, 1.0); break;
+    case 14: k_hbm_write_span<4, true, true><<<grid, 256, 0, s>>>(dst, n / 2, 1.0); break;
+    case 15: k_hbm_write_span<4, false, true><<<grid, 256, 0, s>>>(dst, n / 2, 1.0); break;
+    case 16: k_hbm_write_span<1, true, false><<<grid, 256, 0, s>>>(dst, n / 2, 1.0); break;
+    case 17: k_hbm_write_span<1, false, false><<<grid, 256, 0, s>>>(dst, n / 2, 1.0); break;
+    case 18: k_hbm_write_span<4, false, false><<<grid / 2, 256, 0, s>>>(dst, n / 2, 1.0); break;
+    case 19: k_hbm_write_span<4, false, false><<<grid * 2, 256, 0, s>>>(dst, n / 2, 1.0); break;
+    default: return fail(FA_E_ARG, "mode %d", mode);
+  }
+  LAUNCH_CHECK();
+  return FA_OK;
+}
+
+// Re-check a plan's affine flag against the mesh's current coordinates (a caller that moved the
+// vertices after planning): clears FA_PLAN_AFFINE when a tensor cell is no longer a parallelogram /
+// parallelepiped, sets it when every cell is. Synchronises `stream`.
+extern "C" int fa_plan_check_affine(const fa_mesh* mesh, fa_plan* plan, void* stream) {
+  int rc = check_mesh(mesh);
+  if (rc) return rc;
+  if (!plan) return fail(FA_E_ARG, "null plan");
+  if (!(mesh->cell_type == FA_HEXAHEDRON || mesh->cell_type == FA_QUADRILATERAL) || mesh->ncells == 0) return FA_OK;
+  hipStream_t s = (hipStream_t)stream;
+  MeshView M{mesh->cells, mesh->geom, mesh->x, mesh->ncells, mesh->nnodes, mesh->nn, mesh->nv, mesh->gdim};
+  int* dna = nullptr;
+  int na_h = 1;
+  HIP_TRY(hipMallocAsync((void**)&dna, sizeof(int), s));
+  HIP_TRY(hipMemsetAsync(dna, 0, sizeof(int), s));
+  if (mesh->gdim == 3) k_check_affine<3><<<grid_for(mesh->ncells), 256, 0, s>>>(M, dna);
+  else k_check_affine<2><<<grid_for(mesh->ncells), 256, 0, s>>>(M, dna);
+  LAUNCH_CHECK();
+  HIP_TRY(hipMemcpyAsync(&na_h, dna, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipFreeAsync(dna, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (na_h) plan->cell_flags &= ~FA_PLAN_AFFINE;
+  else plan->cell_flags |= FA_PLAN_AFFINE;
+  return FA_OK;
+}

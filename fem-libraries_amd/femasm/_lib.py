@@ -102,6 +102,7 @@ SIGNATURES = {
     "fa_plan_slots": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_plan_order": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_plan_locality": (ctypes.c_int, [P, P, P, P, P]),
+    "fa_plan_check_affine": (ctypes.c_int, [P, P, P]),
     "fa_plan_gather_contrib": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_plan_contrib_bytes": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_plan_contrib": (ctypes.c_int, [P, P, P, P, I64, P, P]),
@@ -115,6 +116,7 @@ SIGNATURES = {
     "fa_set_bc": (ctypes.c_int, [P, I64, P, P, P, D, P]),
     "fa_bsr_mult": (ctypes.c_int, [P, P, P, P]),
     "fa_bsr_block_diag": (ctypes.c_int, [P, P, P]),
+    "fa_hbm_probe": (ctypes.c_int, [I32, P, P, I64, P]),
 }
 
 _lib = None

@@ -358,14 +358,36 @@ def dirichletbc(value, nodes: torch.Tensor, V: FunctionSpace, components=None) -
     return DirichletBC(V, dofs, g)
 
 
-def _combine_bcs(V: FunctionSpace, bcs):
+def _bcs_key(V: FunctionSpace, bcs, with_g: bool):
+    # identity + storage + in-place version of every input tensor: an edited bc misses the cache
+    parts = [with_g]
+    for bc in bcs:
+        parts.append((id(bc), bc.dofs.data_ptr(), bc.dofs.numel(), bc.dofs._version))
+        if with_g:
+            parts.append((bc.g.data_ptr(), bc.g._version))
+    return tuple(parts)
+
+
+def _combine_bcs(V: FunctionSpace, bcs, with_g: bool = True):
+    """(marker int8 [num_dofs], g f64 [num_dofs] or None) of a bcs list, cached on V per bcs set
+    (a Newton loop assembles with the same bcs every iteration: the marker is built once, not in
+    every timed assembly). with_g=False: the matrix assembly needs the marker only."""
     if not bcs:
         return None, None
+    cache = V.__dict__.setdefault("_bc_cache", {})
+    key = _bcs_key(V, bcs, with_g)
+    hit = cache.get(key)
+    if hit is not None:
+        return hit[0], hit[1]
     marker = torch.zeros(V.num_dofs, dtype=torch.int8, device=V.mesh.device)
-    g = torch.zeros(V.num_dofs, dtype=torch.float64, device=V.mesh.device)
+    g = torch.zeros(V.num_dofs, dtype=torch.float64, device=V.mesh.device) if with_g else None
     for bc in bcs:
         marker[bc.dofs] = 1
-        g[bc.dofs] = bc.g[bc.dofs]
+        if with_g:
+            g[bc.dofs] = bc.g[bc.dofs]
+    if len(cache) >= 8:  # a handful of bcs sets per space; drop the oldest
+        cache.pop(next(iter(cache)))
+    cache[key] = (marker, g, list(bcs))  # the bcs stay referenced: their ids cannot be reused
     return marker, g
 
 
@@ -580,7 +602,30 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.
                 eadj = _plan_order(V, fm, adj, fb, plan, sh)
         corder = _plan_locality(V, fm, adj, plan, sh)
         plans[key] = (plan, rs, A.indptr, slots, eadj, corder)
-    return plans[key][0]
+        V.__dict__.setdefault("_plan_xver", {})[key] = _coords_version(V.mesh)
+    plan = plans[key][0]
+    _recheck_affine(V, key, plan)
+    return plan
+
+
+def _coords_version(m) -> tuple:
+    return (m.x.data_ptr(), m.x._version)
+
+
+def _recheck_affine(V: FunctionSpace, key, plan):
+    """The plan's FA_PLAN_AFFINE flag describes the coordinates it was planned on: the affine tensor
+    gather builds each cell's Jacobian from three edges, so vertices moved in place since then
+    (mesh.x is a public tensor) re-run the library's per-cell affinity check before assembling."""
+    if V.mesh.cell_type not in (CellType.quadrilateral, CellType.hexahedron):
+        return
+    vers = V.__dict__.setdefault("_plan_xver", {})
+    now = _coords_version(V.mesh)
+    if vers.get(key) == now:
+        return
+    fm = V._fa_mesh()
+    _lib.check(_lib.load().fa_plan_check_affine(ctypes.byref(fm), ctypes.byref(plan),
+                                                _lib.stream_handle(V.mesh.device)), "fa_plan_check_affine")
+    vers[key] = now
 
 
 def assemble_matrix(a, bcs=None, diagonal: float = 1.0, A: MatrixCSR | None = None, method: str = "gather") -> MatrixCSR:
@@ -594,7 +639,7 @@ def assemble_matrix(a, bcs=None, diagonal: float = 1.0, A: MatrixCSR | None = No
     if A is None:
         A = create_matrix(a)
     L = _lib.load()
-    marker, _ = _combine_bcs(V, bcs)
+    marker, _ = _combine_bcs(V, bcs, with_g=False)
     fm = V._fa_mesh()
     ff = _fa_form(a)
     sh = _lib.stream_handle(V.mesh.device)
@@ -626,7 +671,7 @@ class SplitGather:
         V = a.V
         L = _lib.load()
         self.L, self.a, self.A, self.diagonal = L, a, A, float(diagonal)
-        self.marker, _ = _combine_bcs(V, bcs)
+        self.marker, _ = _combine_bcs(V, bcs, with_g=False)
         self.fm, self.ff, self.adj = V._fa_mesh(), _fa_form(a), V._fa_adjacency()
         dev = V.mesh.device
         self.sh = _lib.stream_handle(dev)

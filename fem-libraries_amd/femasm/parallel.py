@@ -10,15 +10,19 @@ GPU owns a slab of cube layers [k0, k1) of an n_x x n_y x n_z box:
   the two interface planes (z = k0 and z = k1) carry the full global pattern on both neighbours;
 * rows are the lattice planes p*k0 .. p*k1 of the degree-p lattice (a fa_bsr row window); with
   lattice numbering each interface plane is one contiguous slab of BSR values;
-* the only exchange is, per slab boundary, ONE all-reduce(SUM) between the two neighbouring
-  ranks (a 2-rank process group: xGMI is point-to-point, a global all-reduce of all interfaces
-  would be link-bound — SURVEY.md §5) of the interface rows' blocks in or above the plane (the
-  only ones the upper rank contributes to; ``interface_suffix``). Boundaries are processed in two
-  phases (even pairs, then odd pairs) so the collectives of every rank are issued in a compatible
-  order. The interface rows are assembled first and the all-reduces run on RCCL's stream while the
-  interior rows assemble (``SlabProblem.assemble``).
-* interface rows are owned by the lower rank (doc.tex:464), whose copy is complete after the sum;
-  Dirichlet diagonals on interface rows (inserted by both ranks) are reset to `diagonal`.
+* the only exchange is, per slab boundary, ONE one-way transfer from the upper rank to the plane's
+  owner (the lower rank, doc.tex:464) of the interface rows' blocks in or above the plane -- the
+  only ones the upper rank contributes to (``interface_suffix``) -- which the owner adds into its
+  rows (PETSc's stash does the same at MatAssemblyEnd: off-process entries travel to their owner
+  only). It runs as an RCCL send/recv on a 2-rank process group (xGMI is point-to-point, a global
+  collective over all interfaces would be link-bound -- SURVEY.md §5). Every interior rank sends
+  down one link while it receives from above on another. The interface rows are assembled first
+  and the transfers run on RCCL's streams while the interior rows assemble (``SlabProblem.assemble``).
+  exchange="suffix" keeps the earlier 2-rank all-reduce of the same blocks (both copies complete,
+  twice the link bytes), exchange="rows" all-reduces whole interface rows.
+* the owner's copy is complete after the add; the upper rank's copy of that plane holds only its
+  own partial sums (it owns none of those rows). Dirichlet diagonals on interface rows (inserted
+  by both ranks) are reset to `diagonal`.
 
 The partition / numbering logic (``SlabPartition``) and the exchange (``exchange_interfaces``) are
 device-agnostic (torch tensors on any device, any torch.distributed backend: tested with gloo on
@@ -142,16 +146,21 @@ def bc_diagonal_fixups(part: SlabPartition, indptr: torch.Tensor, indices: torch
 
 
 def exchange_interfaces(part: SlabPartition, values: torch.Tensor, slices: dict, groups, fixups=None,
-                        diagonal: float = 1.0, async_op: bool = False, suffix: dict | None = None):
-    """Sum the interface-plane rows with the slab neighbours (2-rank all-reduces), then reset the
-    Dirichlet diagonals of interface rows. `values` = the window's [nblocks_window, bs, bs].
+                        diagonal: float = 1.0, async_op: bool = False, suffix: dict | None = None,
+                        oneway: bool = False):
+    """Combine the interface-plane rows with the slab neighbours, then reset the Dirichlet diagonals
+    of interface rows. `values` = the window's [nblocks_window, bs, bs].
 
-    suffix (``interface_suffix``): sum only the blocks the rank above a plane contributes to,
-    gathered into a contiguous buffer; the owner's rows are then complete (the non-owner's copy
-    of a plane keeps only that part). None: all-reduce whole interface rows (both copies equal).
-    async_op: only issue the all-reduces (RCCL runs them on its own stream, after the work
-    already queued on the current stream) and return a handle for ``finish_exchange``; the
-    caller can queue the interior rows meanwhile."""
+    oneway (needs `suffix`): the rank above each plane sends its blocks in or above the plane
+    (``interface_suffix``) to the plane's owner, the rank below, which adds them into its rows: the
+    owner's rows are complete, the sender's copy keeps its own partial sums. Each rank sends down
+    and receives from above on two different links at once.
+    Otherwise a 2-rank all-reduce per boundary: of those suffix blocks (`suffix`; the owner's rows
+    complete, the non-owner's copy holds the summed suffix) or of whole interface rows (`suffix`
+    None; both copies equal).
+    async_op: only issue the transfers (RCCL runs them on its own streams, after the work already
+    queued on the current stream) and return a handle for ``finish_exchange``; the caller can queue
+    the interior rows meanwhile."""
     import torch.distributed as dist
 
     flat = values.reshape(values.shape[0], -1)
@@ -160,17 +169,33 @@ def exchange_interfaces(part: SlabPartition, values: torch.Tensor, slices: dict,
         steps.append((part.rank - 1, "lower"))  # boundary q = rank-1
     if part.upper is not None:
         steps.append((part.rank, "upper"))  # boundary q = rank
-    # phase order: even boundaries first, then odd — consistent on both sides of every boundary
     pending = []
-    for q, name in sorted(steps, key=lambda s: (s[0] % 2, s[0])):
-        if suffix is not None:
+    if oneway:
+        if suffix is None:
+            raise ValueError("the one-way exchange sends the interface suffix: pass suffix=interface_suffix(...)")
+        # send the lower plane's suffix down, receive the upper plane's from above (different peers
+        # and links: issued together, no ordering constraint between them)
+        for q, name in steps:
             idx = suffix[name]
-            buf = flat.index_select(0, idx)
-        else:
-            b0, b1 = slices[name]
-            idx, buf = None, flat[b0:b1]
-        w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=groups[q], async_op=async_op)
-        pending.append((w, idx, buf))
+            if name == "lower":
+                buf = flat.index_select(0, idx)
+                w = dist.isend(buf, dst=part.rank - 1, group=groups[q])
+                pending.append((w, None, buf, "send"))
+            else:
+                buf = torch.empty((idx.numel(), flat.shape[1]), dtype=flat.dtype, device=flat.device)
+                w = dist.irecv(buf, src=part.rank + 1, group=groups[q])
+                pending.append((w, idx, buf, "add"))
+    else:
+        # phase order: even boundaries first, then odd -- consistent on both sides of every boundary
+        for q, name in sorted(steps, key=lambda s: (s[0] % 2, s[0])):
+            if suffix is not None:
+                idx = suffix[name]
+                buf = flat.index_select(0, idx)
+            else:
+                b0, b1 = slices[name]
+                idx, buf = None, flat[b0:b1]
+            w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=groups[q], async_op=True)
+            pending.append((w, idx, buf, "copy"))
     handle = (pending, flat, values, fixups, diagonal)
     if async_op:
         return handle
@@ -179,13 +204,17 @@ def exchange_interfaces(part: SlabPartition, values: torch.Tensor, slices: dict,
 
 
 def finish_exchange(handle):
-    """Wait for the all-reduces of ``exchange_interfaces(async_op=True)`` (the current stream waits
-    on RCCL's), scatter gathered sums back and reset the Dirichlet diagonals of the interface rows."""
+    """Wait for the transfers of ``exchange_interfaces(async_op=True)`` (the current stream waits on
+    RCCL's), add / scatter the received blocks and reset the Dirichlet diagonals of the interface rows."""
     pending, flat, values, fixups, diagonal = handle
-    for w, idx, buf in pending:
+    for w, idx, buf, how in pending:
         if w is not None:
             w.wait()
-        if idx is not None:
+        if idx is None:
+            continue
+        if how == "add":
+            flat.index_add_(0, idx, buf)
+        else:
             flat.index_copy_(0, idx, buf)
     if fixups is not None:
         values.view(-1)[fixups] = diagonal
@@ -245,7 +274,7 @@ class SlabProblem:
     owned rows only. ``assemble_residual`` is exchange-mode only."""
 
     def __init__(self, n: int, rank: int, world: int, device, degree: int = 2, nu: float = 0.3, groups=None,
-                 cell_type=None, exchange: str = "suffix", form: str = "linear", qdeg: int | None = None,
+                 cell_type=None, exchange: str = "oneway", form: str = "linear", qdeg: int | None = None,
                  mode: str = "exchange"):
         from . import fem, mesh
         from .la import MatrixCSR
@@ -306,18 +335,29 @@ class SlabProblem:
         inner = (part.row_begin + (part.plane if part.lower else 0), part.row_end - (part.plane if part.upper else 0))
         self.split = fem.SplitGather(self.a, self.bcs, self.A, iface + [inner])
         self.n_iface = len(iface)
+        if exchange not in ("oneway", "suffix", "rows"):
+            raise ValueError(f"unknown exchange {exchange}")
+        self.exchange = exchange
         self.slices = interface_slices(part, self.A.indptr)
-        self.suffix = interface_suffix(part, self.A.indptr, self.A.indices) if exchange == "suffix" else None
+        self.suffix = interface_suffix(part, self.A.indptr, self.A.indices) if exchange != "rows" else None
         bs2 = 9
-        if self.suffix is not None:
+        if exchange == "oneway":  # sent per assembly: the lower plane's suffix (to the rank below)
+            nblk = int(self.suffix["lower"].numel()) if "lower" in self.suffix else 0
+            nrecv = int(self.suffix["upper"].numel()) if "upper" in self.suffix else 0
+        elif self.suffix is not None:  # all-reduced: sent (and received) on each boundary
             nblk = sum(int(v.numel()) for v in self.suffix.values())
+            nrecv = nblk
         else:
             nblk = sum(b1 - b0 for b0, b1 in self.slices.values())
-        self.exchange_bytes = 8 * bs2 * nblk  # values all-reduced per assembly by this rank
+            nrecv = nblk
+        self.exchange_bytes = 8 * bs2 * nblk  # bytes this rank sends per assembly
+        self.exchange_recv_bytes = 8 * bs2 * nrecv  # bytes it receives
         self.fixups = bc_diagonal_fixups(part, self.A.indptr, self.A.indices, marker, 3)
         self.groups = groups if groups is not None else make_pair_groups(world)
-        self.kernel_name = ("k_cell_records + k_gather (interface planes, then interior rows) "
-                            "+ 2-rank all_reduce(SUM) per slab boundary overlapping the interior rows")
+        self.kernel_name = ("k_cell_records + k_gather (interface planes, then interior rows) + per slab "
+                            "boundary " + ("a one-way send of the upper rank's plane blocks to the owner"
+                                           if exchange == "oneway" else "a 2-rank all_reduce(SUM)")
+                            + ", overlapping the interior rows")
 
     def assemble(self, overlap: bool = True):
         """Records of all cells; the interface-plane rows; their 2-rank all-reduces issued on
@@ -332,15 +372,16 @@ class SlabProblem:
         sg.prepare()
         for i in range(self.n_iface):
             sg.rows(i)
+        ow = self.exchange == "oneway"
         if overlap:
             h = exchange_interfaces(self.part, self.A.parts[0][2], self.slices, self.groups, self.fixups,
-                                    async_op=True, suffix=self.suffix)
+                                    async_op=True, suffix=self.suffix, oneway=ow)
             sg.rows(self.n_iface)
             finish_exchange(h)
         else:
             sg.rows(self.n_iface)
             exchange_interfaces(self.part, self.A.parts[0][2], self.slices, self.groups, self.fixups,
-                                suffix=self.suffix)
+                                suffix=self.suffix, oneway=ow)
 
     def assemble_residual(self, f: torch.Tensor | None = None, b: torch.Tensor | None = None) -> torch.Tensor:
         """The reference's setF on this slab (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:817-845):

@@ -179,6 +179,12 @@ int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A,
 int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int32_t* eadj, fa_plan* plan,
                   void* stream);
 
+/* Re-check plan->cell_flags & FA_PLAN_AFFINE against the mesh's CURRENT vertex coordinates (a
+ * caller that moved vertices after fa_plan_gather): the affine tensor gather builds each cell's
+ * Jacobian from three edge vectors, so a plan must not call a cell affine that no longer is.
+ * Synchronises `stream`. A no-op for simplices (always affine). */
+int fa_plan_check_affine(const fa_mesh* mesh, fa_plan* plan, void* stream);
+
 /* Chunk visiting order for cache locality: chunks sorted by the Morton key of a point of each
  * chunk (the centroid of the cell of its first adjacency entry), so that chunks the gather runs
  * close in time share cells and their per-cell records stay in L2. corder is a caller-owned device
@@ -252,6 +258,12 @@ int fa_bsr_mult(const fa_bsr* A, const double* x, double* y, void* stream);
 /* out[r - row_begin] = the diagonal block of block row r (zeros when absent), [rows, bs, bs]:
  * the block-Jacobi preconditioner of the driver's CG (the reference uses BoomerAMG, :717-813). */
 int fa_bsr_block_diag(const fa_bsr* A, double* out, void* stream);
+
+/* Measurement helper (not part of the reference interface): a 16-B-per-lane grid-stride stream
+ * over n doubles (n even, 16-B aligned buffers) for the measured HBM peak beside the 8 TB/s spec
+ * (SURVEY.md section 8(d)). mode 0: dst = src (copy), 1: dst = 1.0 (write only), 2: read src
+ * (dst receives one partial sum per workgroup; n >= 8 * CUs). Asynchronous on `stream`. */
+int fa_hbm_probe(int32_t mode, double* dst, const double* src, int64_t n, void* stream);
 
 #ifdef __cplusplus
 }

@@ -55,8 +55,10 @@ def _worker(rank, world, port, n, kind="linear"):
         lc = ix_l[ip_l[r]:ip_l[r + 1]]
         assert np.array_equal(lc + part.node_offset, ix_g[ip_g[g]:ip_g[g + 1]])
         lv, gv = vl[ip_l[r] - w0:ip_l[r + 1] - w0], vg[ip_g[g]:ip_g[g + 1]]
-        if part.lower is not None and r < part.lower[1]:  # non-owned copy: the exchanged blocks only
-            keep = lc >= part.lower[0]
+        if part.lower is not None and r < part.lower[1]:  # non-owned copy
+            if prob.exchange == "oneway":
+                continue  # the rank's own partial sums, sent to the owner
+            keep = lc >= part.lower[0]  # suffix all-reduce: the exchanged blocks only
             lv, gv = lv[keep], gv[keep]
         err = max(err, float(np.abs(lv - gv).max()))
     assert err <= 1e-12 * scale, f"rank {rank}: rel err {err / scale:.2e}"

@@ -73,12 +73,13 @@ def _worker(rank, world, port, n, async_op=False, mode="rows", kind="linear"):
     slices = parallel.interface_slices(part, ip_t)
     fix = parallel.bc_diagonal_fixups(part, ip_t, ix_t, marker, bs)
     groups = parallel.make_pair_groups(world)
-    suffix = parallel.interface_suffix(part, ip_t, ix_t) if mode == "suffix" else None
+    suffix = parallel.interface_suffix(part, ip_t, ix_t) if mode in ("suffix", "oneway") else None
+    ow = mode == "oneway"
     if async_op:  # the overlapped form SlabProblem.assemble uses: issue, (interior work), finish
-        h = parallel.exchange_interfaces(part, window, slices, groups, fix, async_op=True, suffix=suffix)
+        h = parallel.exchange_interfaces(part, window, slices, groups, fix, async_op=True, suffix=suffix, oneway=ow)
         parallel.finish_exchange(h)
     else:
-        parallel.exchange_interfaces(part, window, slices, groups, fix, suffix=suffix)
+        parallel.exchange_interfaces(part, window, slices, groups, fix, suffix=suffix, oneway=ow)
 
     # global reference
     m = mesh.create_unit_cube(n, n, n, ct)
@@ -98,9 +99,12 @@ def _worker(rank, world, port, n, async_op=False, mode="rows", kind="linear"):
         assert np.array_equal(lc, gc), f"rank {rank} row {r}: pattern differs"
         lv = window[int(indptr[r]) - w0:int(indptr[r + 1]) - w0].numpy()
         gv = gvals[gip[g]:gip[g + 1]]
-        if mode == "suffix" and part.lower is not None and r < part.lower[1]:
-            keep = lc >= part.lower[0] + part.node_offset  # non-owned copy: the exchanged blocks only
-            lv, gv = lv[keep], gv[keep]
+        if part.lower is not None and r < part.lower[1]:
+            if mode == "oneway":
+                continue  # non-owned copy: the rank's own partial sums, sent to the owner
+            if mode == "suffix":
+                keep = lc >= part.lower[0] + part.node_offset  # non-owned copy: the exchanged blocks only
+                lv, gv = lv[keep], gv[keep]
         err = max(err, float(np.abs(lv - gv).max()))
     assert err <= 1e-12 * scale, f"rank {rank}: rel err {err / scale:.2e}"
     dist.destroy_process_group()
@@ -108,16 +112,25 @@ def _worker(rank, world, port, n, async_op=False, mode="rows", kind="linear"):
 
 @pytest.mark.parametrize("world,n,async_op,mode", [(2, 4, False, "rows"), (3, 5, False, "rows"), (4, 4, False, "rows"),
                                                    (3, 5, True, "rows"), (2, 4, False, "suffix"),
-                                                   (4, 4, True, "suffix"), (3, 5, True, "suffix")])
+                                                   (4, 4, True, "suffix"), (3, 5, True, "suffix"),
+                                                   (2, 4, False, "oneway"), (3, 5, True, "oneway"),
+                                                   (4, 4, True, "oneway")])
 def test_slab_exchange_gloo(world, n, async_op, mode):
     mp.spawn(_worker, args=(world, _free_port(), n, async_op, mode), nprocs=world, join=True)
 
 
-@pytest.mark.parametrize("world,n", [(2, 4), (3, 5)])
-def test_slab_exchange_neohookean_gloo(world, n):
+def test_slab_exchange_world8_gloo():
+    """The driver's N = 8 decomposition (one rank per GPU of a node) rehearsed on CPU: 8 gloo ranks,
+    one cube layer each, the one-way interface exchange overlapped; every owned row equals the
+    oracle's global assembly."""
+    mp.spawn(_worker, args=(8, _free_port(), 8, True, "oneway"), nprocs=8, join=True)
+
+
+@pytest.mark.parametrize("world,n,mode", [(2, 4, "suffix"), (3, 5, "suffix"), (3, 5, "oneway")])
+def test_slab_exchange_neohookean_gloo(world, n, mode):
     """Config E's physics on slabs: the neo-Hookean tangent at u = 1e-3 sin(pi x) (oracle closed form
-    per rank), suffix exchange overlapped: owned rows equal the global assembly."""
-    mp.spawn(_worker, args=(world, _free_port(), n, True, "suffix", "neo"), nprocs=world, join=True)
+    per rank), exchange overlapped: owned rows equal the global assembly."""
+    mp.spawn(_worker, args=(world, _free_port(), n, True, mode, "neo"), nprocs=world, join=True)
 
 
 def _residual_worker(rank, world, port, n, kind):
