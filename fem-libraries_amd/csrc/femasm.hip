@@ -174,6 +174,7 @@ struct MeshView {
 
 struct FormView {
   int kind;
+  int ad;  // FA_ASYM_DAMAGE_AD: the damage law's tangent and stress by AD of its potential (USE_AD)
   const double* E;
   double nu;
   const double* lam;
@@ -328,6 +329,132 @@ __device__ __forceinline__ void lin_block(const double (&G)[GD][GD], double lam,
     for (int j = 0; j < GD; ++j) K[i][j] = (i == j) ? fma(lm, G[i][i], mtr) : fma(mu, G[j][i], lam * G[i][j]);
 }
 
+// ------------------------------------------------------------------------------------ AD: dual numbers
+// Forward-mode dual numbers, nested for second derivatives: the Hessian of a potential psi(F) is
+// taken entry by entry over the upper triangle, seeding x_i in the inner and x_j in the outer
+// level (the forward-over-forward pattern of the reference's MFEM AD,
+// MFEM/mechanic2d/autodiff/admfem.hpp:672-700: n(n+1)/2 evaluations; here n = gdim^2).
+template <class T>
+struct Dual {
+  T v, d;
+};
+template <class T>
+__device__ __forceinline__ Dual<T> operator+(const Dual<T>& a, const Dual<T>& b) { return {a.v + b.v, a.d + b.d}; }
+template <class T>
+__device__ __forceinline__ Dual<T> operator-(const Dual<T>& a, const Dual<T>& b) { return {a.v - b.v, a.d - b.d}; }
+template <class T>
+__device__ __forceinline__ Dual<T> operator*(const Dual<T>& a, const Dual<T>& b) { return {a.v * b.v, a.d * b.v + a.v * b.d}; }
+template <class T>
+__device__ __forceinline__ Dual<T> operator*(double s, const Dual<T>& a) { return {s * a.v, s * a.d}; }
+template <class T>
+__device__ __forceinline__ Dual<T> operator+(const Dual<T>& a, double s) { return {a.v + s, a.d}; }
+__device__ __forceinline__ double ad_inv(double x) { return 1.0 / x; }
+template <class T>
+__device__ __forceinline__ Dual<T> ad_inv(const Dual<T>& a) {
+  T r = ad_inv(a.v);
+  return {r, (-1.0) * (a.d * r * r)};
+}
+__device__ __forceinline__ double ad_log(double x) { return log(x); }
+template <class T>
+__device__ __forceinline__ Dual<T> ad_log(const Dual<T>& a) { return {ad_log(a.v), a.d * ad_inv(a.v)}; }
+
+__device__ __forceinline__ double ad_sqrt(double x) { return sqrt(x); }
+template <class T>
+__device__ __forceinline__ Dual<T> ad_sqrt(const Dual<T>& a) {
+  T r = ad_sqrt(a.v);
+  return {r, 0.5 * (a.d * ad_inv(r))};
+}
+__device__ __forceinline__ double ad_val(double x) { return x; }
+template <class T>
+__device__ __forceinline__ double ad_val(const Dual<T>& a) { return ad_val(a.v); }
+
+// The reference's asymmetric damage potential psi(strain; lam, mu, d) (MFEM/mechanic2d/
+// asym_elasto_damage_model.cc:100-155, the functor its USE_AD build differentiates), strain state
+// (e11, e21, e12, e22): lam/2 I1^2 (1 - alpha d) + mu sum_k (1 - alpha_k d) ev_k^2 with the
+// principal strains ev_k and alpha = [I1 >= 0], alpha_k = [ev_k >= 0] (branch tests on the primal
+// values, as the AD types compare); the "null tensor" branch is the linear potential scaled by 1 - d.
+template <class T>
+__device__ __forceinline__ T damage_potential(const T (&e)[4], double l, double m, double d) {
+  const double limit = 1.e-12, mlimit = -1.e-12;
+  const T I1 = e[0] + e[3];
+  const T I2 = e[1] * e[2] - e[0] * e[3];
+  const double i1 = ad_val(I1), i2 = ad_val(I2);
+  if (i1 > limit || i2 > limit || i1 < mlimit || i2 < mlimit) {
+    const T delta = I1 * I1 + 4.0 * I2;
+    const T r = ad_sqrt(delta);
+    const T ev1 = 0.5 * (I1 + r), ev2 = 0.5 * (I1 - r);
+    const double alpha1 = ad_val(ev1) >= 0.0 ? 1.0 : 0.0, alpha2 = ad_val(ev2) >= 0.0 ? 1.0 : 0.0;
+    const double alpha = (ad_val(ev1) + ad_val(ev2)) >= 0.0 ? 1.0 : 0.0;
+    return (0.5 * (1.0 - alpha * d) * l) * (I1 * I1) +
+           m * ((1.0 - alpha1 * d) * (ev1 * ev1) + (1.0 - alpha2 * d) * (ev2 * ev2));
+  }
+  return (1.0 - d) * ((0.5 * l) * (I1 * I1) + m * (e[0] * e[0] + e[3] * e[3] + e[1] * e[1] + e[2] * e[2]));
+}
+
+// USE_AD tangent (MFEM/mechanic2d/asym_elasto_damage_model.cc:735-765): for d > 0 (limited to
+// 1 - 1e-12) the Hessian of damage_potential over the 4 strain components by forward-over-forward
+// AD, upper triangle (admfem.hpp:672-700: n(n+1)/2 = 10 passes), reordered to Voigt (xx, yy, xy):
+// hook(i, j) = hess(i + 2 (i % 2), j + 2 (j % 2)), hook(2, 2) = (hess(2, 2) + hess(1, 2)) / 2
+// (:761-763). d = 0 keeps the linear branch (:873-881), as the reference never differentiates there.
+__device__ __noinline__ void damage_hook_ad(double s00, double s11, double s01, double l, double m, double d,
+                                            double (&H)[3][3]) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) H[i][j] = 0.0;
+  if (!(d > 0.0)) {
+    H[0][0] = H[1][1] = 2.0 * m + l;
+    H[0][1] = H[1][0] = l;
+    H[2][2] = m;
+    return;
+  }
+  d = fmin(d, 1.0 - 1.e-12);
+  const double st[4] = {s00, s01, s01, s11};  // column-major strain: e11, e21, e12, e22
+  using DD = Dual<Dual<double>>;
+  double hs[4][4];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j <= i; ++j) {
+      DD x[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x[k] = DD{{st[k], k == i ? 1.0 : 0.0}, {k == j ? 1.0 : 0.0, 0.0}};
+      const double h = damage_potential<DD>(x, l, m, d).d.d;
+      hs[i][j] = h;
+      hs[j][i] = h;
+    }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) H[i][j] = hs[i + 2 * (i % 2)][j + 2 * (j % 2)];
+  H[2][2] = 0.5 * (H[2][2] + hs[1][2]);
+}
+
+// USE_AD stress (asym_stress, :158-204): for d > 0 the gradient of damage_potential with the Lame
+// parameters scaled by w (4 forward-mode passes), sig = [[g_e11, g_e12], [g_e21, g_e22]]; d = 0 the
+// linear stress.
+__device__ __noinline__ void damage_stress_ad(double s00, double s11, double s01, double l, double m, double d,
+                                              double w, double (&sig)[2][2]) {
+  if (!(d > 0.0)) {
+    const double m2plw = w * (2.0 * m + l), lw = l * w;
+    sig[0][0] = m2plw * s00 + lw * s11;
+    sig[1][1] = m2plw * s11 + lw * s00;
+    sig[0][1] = sig[1][0] = w * m * (s01 + s01);
+    return;
+  }
+  const double st[4] = {s00, s01, s01, s11};
+  using D1 = Dual<double>;
+  double g[4];
+  for (int i = 0; i < 4; ++i) {
+    D1 x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = D1{st[k], k == i ? 1.0 : 0.0};
+    g[i] = damage_potential<D1>(x, l * w, m * w, d).d;
+  }
+  sig[0][0] = g[0];
+  sig[1][0] = g[1];
+  sig[0][1] = g[2];
+  sig[1][1] = g[3];
+}
+
 // Reference damage-law tangent "hook" (Voigt xx, yy, xy-engineering), restated from MFEM
 // damIntegrator::AssembleElementGrad (MFEM/mechanic2d/asym_elasto_damage_model.cc:728-881).
 __device__ __forceinline__ void damage_hook(double s00, double s11, double s01, double l, double m, double d,
@@ -414,7 +541,8 @@ __device__ __forceinline__ void damage_cell(const MeshView& M, const FormView& F
     if (F.d) dq += F.d[n];
   }
   dq *= (1.0 / 3.0);
-  damage_hook(gr[0][0], gr[1][1], 0.5 * (gr[0][1] + gr[1][0]), lam, mu, dq, H);
+  if (F.ad) damage_hook_ad(gr[0][0], gr[1][1], 0.5 * (gr[0][1] + gr[1][0]), lam, mu, dq, H);
+  else damage_hook(gr[0][0], gr[1][1], 0.5 * (gr[0][1] + gr[1][0]), lam, mu, dq, H);
 }
 
 // K_ab = w B_a^T H B_b with B_a = [[gx,0],[0,gy],[gy,gx]] (MFEM USE_B, :699-704, :885-887)
@@ -446,35 +574,6 @@ __device__ __forceinline__ int64_t find_slot(const int64_t* indptr, const int32_
   }
   return -1;
 }
-
-// ------------------------------------------------------------------------------------ AD: neo-Hookean tangent
-// Forward-mode dual numbers, nested for second derivatives: the Hessian of a potential psi(F) is
-// taken entry by entry over the upper triangle, seeding x_i in the inner and x_j in the outer
-// level (the forward-over-forward pattern of the reference's MFEM AD,
-// MFEM/mechanic2d/autodiff/admfem.hpp:672-700: n(n+1)/2 evaluations; here n = gdim^2).
-template <class T>
-struct Dual {
-  T v, d;
-};
-template <class T>
-__device__ __forceinline__ Dual<T> operator+(const Dual<T>& a, const Dual<T>& b) { return {a.v + b.v, a.d + b.d}; }
-template <class T>
-__device__ __forceinline__ Dual<T> operator-(const Dual<T>& a, const Dual<T>& b) { return {a.v - b.v, a.d - b.d}; }
-template <class T>
-__device__ __forceinline__ Dual<T> operator*(const Dual<T>& a, const Dual<T>& b) { return {a.v * b.v, a.d * b.v + a.v * b.d}; }
-template <class T>
-__device__ __forceinline__ Dual<T> operator*(double s, const Dual<T>& a) { return {s * a.v, s * a.d}; }
-template <class T>
-__device__ __forceinline__ Dual<T> operator+(const Dual<T>& a, double s) { return {a.v + s, a.d}; }
-__device__ __forceinline__ double ad_inv(double x) { return 1.0 / x; }
-template <class T>
-__device__ __forceinline__ Dual<T> ad_inv(const Dual<T>& a) {
-  T r = ad_inv(a.v);
-  return {r, (-1.0) * (a.d * r * r)};
-}
-__device__ __forceinline__ double ad_log(double x) { return log(x); }
-template <class T>
-__device__ __forceinline__ Dual<T> ad_log(const Dual<T>& a) { return {ad_log(a.v), a.d * ad_inv(a.v)}; }
 
 // Compressible neo-Hookean potential psi(F) = mu/2 (I_C - 3) - mu ln J + lam/2 (ln J)^2,
 // F = I + grad u (2-D: plane strain, F33 = 1, so I_C - 3 = F:F - 2).
@@ -1081,6 +1180,7 @@ struct GatherArgs {
   const int64_t* chunk_a;  // [nchunks + 1] adj_ptr[row_start[c]]
   int64_t nchunks;
   int32_t plan_maxb;        // largest block count of a chunk of the plan (checked against the kernel's)
+  int32_t plan_maxadj;      // largest adjacency count of a chunk of the plan
   unsigned long long* ctr;  // [8] per-XCD chunk counters (dynamic persistent grid), or NULL
   const uint16_t* slots;  // optional [adjacency entry][NN] position of the block within its row
   int slot_order;         // 0, or the NSPLIT whose item order fa_plan_order baked into `slots`
@@ -2747,6 +2847,254 @@ void k_gather(GatherArgs P) {
 #endif
 }
 
+// ------------------------------------------------------------------------------ store-decoupled gather
+// k_gather_lin: the uniform-nu affine-simplex gather (MAT_LINU: configs A, C, E) with a positional
+// plan, written so that a workgroup never waits for its own chunk stores. CDNA counts stores in
+// vmcnt, and a wave's wait for a load also waits for every older vector-memory operation: in
+// k_gather a chunk's item loads were issued after the previous chunk's stores, so every chunk's
+// compute started only once those stores had drained (and its register spills waited vmcnt(0)).
+// Here every vector-memory operation of the loop is unconditional and of a static count per lane
+// (clamped addresses; lanes past a chunk's items or values repeat a valid load / store of the same
+// value), so the compiler's vmcnt waits count exactly the operations issued after a load, and the
+// loads of chunk k+1 (its entries two chunks ahead, its records / slots / masks one chunk ahead)
+// are issued BEFORE chunk k's stores: the item phase of chunk k+1 waits for its own data only,
+// while chunk k's 27 KB drain behind it (each workgroup keeps two chunks of stores in flight).
+// Per chunk: items (LDS atomics; the reference-tensor table B_ab read one block ahead so the wait
+// for it never includes the previous block's atomics) | barrier | accumulator read into registers
+// | barrier | zero what was read, 16-B non-temporal stores (+ the unpaired head / tail value) |
+// barrier. Chunks are a static contiguous range per workgroup (no chunk counter: its atomic would
+// be a conditional vector-memory operation), XCD-contiguous. Dirichlet diagonals are set after the
+// launch (k_bc_diag), items zero every constrained entry as in k_gather. Plans: <= 256 items per
+// chunk (fa_plan_gather caps a chunk at 256 / NSPLIT adjacency entries for these elements).
+#ifndef FA_LIN_ABL
+// timing-only ablations of k_gather_lin (wrong results; tools/lin_ablate.sh): 1 plain read-add-write
+// instead of LDS atomics (races), 2 no accumulator adds, 3 no table reads, 4 no chunk stores,
+// 5 no item loads (constant records / slots)
+#define FA_LIN_ABL 0
+#endif
+template <int GD, int NN, int NSPLIT>
+__global__ __launch_bounds__(256, 4) void k_gather_lin(GatherArgs P, const uint32_t* __restrict__ zero32,
+                                                        double* __restrict__ dump, int64_t per) {
+  using R = Rec<GD, GD + 1, 1, MAT_LINU>;
+  constexpr int BS2 = GD * GD;
+  constexpr int NBG = NN / NSPLIT;
+  constexpr int MAXB = gather_maxb(false, BS2);
+  constexpr int NACC = MAXB * BS2 + 2;       // value p of a chunk at acc[p + h], h = its parity
+  constexpr int NP2 = (NACC + 1) / 2;        // 16-B pairs of the accumulator
+  constexpr int SW = (MAXB * BS2 / 2 + 255) / 256;  // pair stores per lane per chunk
+  constexpr int RL = R::SIZE;
+  static_assert(NN % NSPLIT == 0 && NN * GD <= 32 && RL % 2 == 0 && NN <= 63, "k_gather_lin: affine simplices");
+  typedef double dv2 __attribute__((ext_vector_type(2)));
+  __shared__ __attribute__((aligned(16))) double acc[2 * NP2];
+  __shared__ double tab[NN * NN * BS2];
+  dv2* acc2 = reinterpret_cast<dv2*>(acc);
+  const int tid = threadIdx.x;
+  const int G = gridDim.x;  // a multiple of 8
+  const int64_t wg = (int64_t)(blockIdx.x % 8) * (G / 8) + blockIdx.x / 8;
+  const int64_t c_begin = min(wg * per, P.nchunks), c_end = min(c_begin + per, P.nchunks);
+  if (c_begin >= c_end) return;  // the whole workgroup
+  for (int t = tid; t < NN * NN * BS2; t += 256) tab[t] = P.ahat[t];
+  for (int t = tid; t < NP2; t += 256) acc2[t] = dv2{0.0, 0.0};
+
+  const int64_t abase = sload(P.A.indptr, P.A.row_begin);
+  const int64_t nent = P.M.ncells * NN;
+  const int32_t* __restrict__ eadj = P.eadj;
+  const uint32_t* __restrict__ mk = P.bcmask ? P.bcmask : zero32;
+  const uint32_t mkmul = P.bcmask ? 1u : 0u;
+  struct Desc { int64_t b0, b1, a0, a1; };
+  auto desc = [&](int64_t c) -> Desc {  // clamped to the workgroup's last chunk: static loads
+    c = min(c, c_end - 1);
+    const int64_t r0 = sload(P.row_start, c), r1 = sload(P.row_start, c + 1);
+    return Desc{sload(P.A.indptr, r0), sload(P.A.indptr, r1), sload(P.adj_ptr, r0), sload(P.adj_ptr, r1)};
+  };
+  const int jit = tid / NSPLIT, part = tid % NSPLIT;
+  // entry id (cell * NN + local row node) of this lane's item, clamped to a valid entry
+  auto load_entry = [&](const Desc& d) -> int32_t {
+    const int na = (int)(d.a1 - d.a0);
+    int64_t e = d.a0 + min(jit, max(na - 1, 0));
+    e = min(max(e, (int64_t)0), nent - 1);
+    return eadj[e];
+  };
+  struct Item { double r[RL]; uint32_t sl[NBG]; uint32_t mask; };
+  auto load_item = [&](const Desc& d, int32_t pflat, Item& it) {
+    const int64_t c = pflat / NN;
+#if FA_LIN_ABL == 5
+#pragma unroll
+    for (int k = 0; k < RL; ++k) it.r[k] = 0.5 + 0.01 * k + 1e-9 * (double)c;
+    const int na5 = (int)(d.a1 - d.a0);
+#pragma unroll
+    for (int bb = 0; bb < NBG; ++bb) it.sl[bb] = ((uint32_t)((part * NBG + bb) % NN) << 10) | (uint32_t)((jit * 7 + bb * 13) % max(na5, 1));
+    it.mask = 0u;
+    return;
+#endif
+    const dv2* rp = reinterpret_cast<const dv2*>(P.rec + c * RL);
+#pragma unroll
+    for (int k = 0; k < RL / 2; ++k) {
+      const dv2 v = rp[k];
+      it.r[2 * k] = v.x;
+      it.r[2 * k + 1] = v.y;
+    }
+    const int na = (int)(d.a1 - d.a0);
+    int64_t e = d.a0 + min(jit, max(na - 1, 0));
+    e = min(max(e, (int64_t)0), nent - 1);
+    const uint16_t* sp = P.slots + e * NN + part * NBG;
+#pragma unroll
+    for (int bb = 0; bb < NBG; ++bb) it.sl[bb] = sp[bb];
+    it.mask = mk[c * mkmul] * mkmul;
+  };
+
+  Desc d0 = desc(c_begin), d1 = desc(c_begin + 1), d2 = desc(c_begin + 2);
+  int32_t pf0 = load_entry(d0), pf1 = load_entry(d1);
+  Item cur, nxt;
+  load_item(d0, pf0, cur);
+  int bad = 0;
+  // the prologue's loads complete here (a builtin wait: the compiler's wait counting sees it, so the
+  // loop's waits are not widened by pending prologue loads merged in at the loop head)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();  // table and accumulator staged
+  for (int64_t k = c_begin; k < c_end; ++k) {
+    // L1: chunk k+2's entry ids; L2: chunk k+1's records / slots / masks (before chunk k's stores)
+    const int32_t pf2 = load_entry(d2);
+    load_item(d1, pf1, nxt);
+    const Desc d3 = desc(k + 3);
+    // items of chunk k
+    const int64_t off = (d0.b0 - abase) * BS2;
+    const int h = (int)(off & 1);
+    const int nb = (int)(d0.b1 - d0.b0);
+    const bool valid = jit < (int)(d0.a1 - d0.a0);
+    {
+      const int aloc = pf0 % NN;
+      const double* Ah0 = tab + aloc * NN * BS2;
+      const uint32_t rowm = (cur.mask >> (aloc * GD)) & ((1u << GD) - 1);
+      const bool negw = __any(cur.r[BS2] < 0.0);  // wave-uniform: a cell with mu |J| < 0
+      double Bn[BS2];
+      {
+        const int b = (int)(cur.sl[0] >> 10);
+#pragma unroll
+        for (int e = 0; e < BS2; ++e) Bn[e] = Ah0[b * BS2 + e];
+      }
+#pragma unroll
+      for (int bb = 0; bb < NBG; ++bb) {
+        const int s = (int)(cur.sl[bb] & 1023u);
+        const int b = (int)(cur.sl[bb] >> 10);
+        double B[BS2];
+#pragma unroll
+        for (int e = 0; e < BS2; ++e) B[e] = Bn[e];
+        if (bb + 1 < NBG) {  // next block's table entry: issued before this block's atomics
+          const int b1 = (int)(cur.sl[bb + 1 < NBG ? bb + 1 : bb] >> 10);
+#if FA_LIN_ABL == 3
+#pragma unroll
+          for (int e = 0; e < BS2; ++e) Bn[e] = 0.1 * e + b1;
+#else
+#pragma unroll
+          for (int e = 0; e < BS2; ++e) Bn[e] = Ah0[b1 * BS2 + e];
+#endif
+        }
+        // G = (s Ji)^T B (s Ji), column by column; K = G + tr(G) / (1 + r) I
+        double G[GD][GD];
+#pragma unroll
+        for (int dd = 0; dd < GD; ++dd) {
+          double T[GD];
+#pragma unroll
+          for (int i = 0; i < GD; ++i) {
+            double t = B[i * GD] * cur.r[dd];
+#pragma unroll
+            for (int kk = 1; kk < GD; ++kk) t = fma(B[i * GD + kk], cur.r[kk * GD + dd], t);
+            T[i] = t;
+          }
+#pragma unroll
+          for (int e = 0; e < GD; ++e) {
+            double g = cur.r[e] * T[0];
+#pragma unroll
+            for (int i = 1; i < GD; ++i) g = fma(cur.r[i * GD + e], T[i], g);
+            G[e][dd] = g;
+          }
+        }
+        double tr = G[0][0];
+#pragma unroll
+        for (int i = 1; i < GD; ++i) tr += G[i][i];
+        tr *= P.trc;
+#pragma unroll
+        for (int i = 0; i < GD; ++i) G[i][i] += tr;
+        if (negw) {
+          const double sg = cur.r[BS2];
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int kk = 0; kk < GD; ++kk) G[i][kk] *= sg;
+        }
+        const uint32_t colm = (cur.mask >> (b * GD)) & ((1u << GD) - 1);
+        if (__any((rowm | colm) != 0u)) {
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int kk = 0; kk < GD; ++kk)
+              if (((rowm >> i) | (colm >> kk)) & 1u) G[i][kk] = 0.0;
+        }
+        bad |= valid && s >= nb;
+        if (valid && s < nb) {
+          double* ap = acc + h + s * BS2;
+#if FA_LIN_ABL == 1
+          double o[BS2];
+#pragma unroll
+          for (int e = 0; e < BS2; ++e) o[e] = ap[e];
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int kk = 0; kk < GD; ++kk) ap[i * GD + kk] = o[i * GD + kk] + G[i][kk];
+#elif FA_LIN_ABL == 2
+          if (G[0][0] == 1.2345e-300) ap[0] = G[1][1];
+#else
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int kk = 0; kk < GD; ++kk) atomicAdd(ap + i * GD + kk, G[i][kk]);
+#endif
+        }
+      }
+    }
+    __syncthreads();  // B1: the chunk is accumulated
+    // read the chunk into registers: pairs t (value 2t + h .. 2t + 1 + h at acc2[t + h]); lanes past
+    // the chunk's pairs repeat the last pair, and every lane reads the unpaired head / tail value
+    const int nv = nb * BS2;
+    const int np = (nv - h) >> 1;
+    dv2 v[SW];
+#pragma unroll
+    for (int u = 0; u < SW; ++u) v[u] = acc2[h + max(min(tid + 256 * u, np - 1), 0)];
+    const double hv = acc[h], tv = acc[max(nv - 1, 0) + h];
+    __syncthreads();  // B2: every read is done before any zero
+#pragma unroll
+    for (int u = 0; u < SW; ++u)
+      if (tid + 256 * u < np) acc2[h + tid + 256 * u] = dv2{0.0, 0.0};
+    // the unpaired head (acc[1] when h = 1) and tail sit in pairs whose other half is never written
+    if (tid == 0) acc2[0] = dv2{0.0, 0.0};
+    if (tid == 1) acc2[(max(nv - 1, 0) + h) >> 1] = dv2{0.0, 0.0};
+    // stores: SW pair stores + the head and the tail value, on every lane (repeats write the same
+    // value to the same address)
+    // a chunk without values (rows of no cell) stores its repeats into a scratch line instead
+    const bool none = np < 1;
+    double* out = none ? dump : P.A.data + off;
+    dv2* out2 = reinterpret_cast<dv2*>(none ? dump : out + h);
+#if FA_LIN_ABL == 4
+    if (hv == 1.2345e-300) out[0] = tv + v[0].x + v[SW - 1].y;
+#else
+#pragma unroll
+    for (int u = 0; u < SW; ++u) __builtin_nontemporal_store(v[u], out2 + max(min(tid + 256 * u, np - 1), 0));
+    __builtin_nontemporal_store(hv, out);
+    __builtin_nontemporal_store(tv, out + max(nv - 1, 0));
+#endif
+    __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics
+    // rotate the pipeline
+    d0 = d1;
+    d1 = d2;
+    d2 = d3;
+    pf0 = pf1;
+    pf1 = pf2;
+    cur = nxt;
+  }
+  if (bad) atomicOr(P.err, 1);
+}
+
 // ------------------------------------------------------------------------------ block-owner gather
 // k_gather_own: the uniform-nu affine-simplex gather (MAT_LINU) without per-contribution LDS
 // atomics. The contribution plan (fa_plan_contrib) lists, per chunk, every (cell, row node a,
@@ -3859,11 +4207,21 @@ static int plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bs
   return FA_OK;
 }
 
+static bool lin_gather_enabled();
 extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int64_t* row_start,
                               fa_plan* plan, void* stream) {
   if (!mesh) return fail(FA_E_ARG, "null mesh");
-  return plan_gather(mesh, adj, A, row_start, plan, stream, gather_maxb(false, mesh->gdim * mesh->gdim),
-                     std::min(FA_GATHER_ENTRY_CAP, kGatherMaxAdj));
+  int maxadj = std::min(FA_GATHER_ENTRY_CAP, kGatherMaxAdj);
+  // simplices of the affine elasticity kernels: chunks of at most 256 items (k_gather_lin's one item
+  // per lane), i.e. 256 / NSPLIT adjacency entries
+  if (mesh->cell_type == FA_TRIANGLE || mesh->cell_type == FA_TETRAHEDRON) {
+    DevTables T;
+    int rc = get_tables(mesh->cell_type, mesh->degree, -1, &T);
+    if (rc) return rc;
+    const int ns = lin_simplex_nsplit(mesh->cell_type, mesh->degree, T.nq);
+    if (ns > 0 && lin_gather_enabled()) maxadj = std::min(maxadj, 256 / ns);
+  }
+  return plan_gather(mesh, adj, A, row_start, plan, stream, gather_maxb(false, mesh->gdim * mesh->gdim), maxadj);
 }
 
 extern "C" int fa_plan_gather_form(const fa_mesh* mesh, int32_t kind, const fa_adjacency* adj, const fa_bsr* A,
@@ -4215,6 +4573,11 @@ extern "C" int fa_plan_locality(const fa_mesh* mesh, const fa_adjacency* adj, in
 static int form_view(const fa_mesh* mesh, const fa_form* form, FormView& F) {
   if (!form) return fail(FA_E_ARG, "null form");
   F.kind = form->kind;
+  F.ad = 0;
+  if (F.kind == FA_ASYM_DAMAGE_AD) {  // the damage law with the USE_AD tangent and stress
+    F.kind = FA_ASYM_DAMAGE;
+    F.ad = 1;
+  }
   F.E = form->E;
   F.nu = form->nu;
   F.lam = form->lam;
@@ -4326,6 +4689,31 @@ __global__ void k_bhat(const double* __restrict__ ahat, int nblk, double r, doub
         bhat[t * GD * GD + i * GD + k] = r * ahat[t * GD * GD + i * GD + k] + ahat[t * GD * GD + k * GD + i];
 }
 
+// FEMASM_LIN_GATHER=0: the affine-simplex elasticity plans run k_gather instead of k_gather_lin
+static bool lin_gather_enabled() {
+  const char* e = getenv("FEMASM_LIN_GATHER");
+  return !(e && e[0] == '0');
+}
+
+// k_gather_lin's constant operands: a zero mask word (no bcs) and a scratch line for the stores of
+// a chunk without values; allocated once per process
+static int lin_scratch(uint32_t** zero32, double** dump) {
+  static uint32_t* z = nullptr;
+  static double* d = nullptr;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!z) {
+    void* p = nullptr;
+    HIP_TRY(hipMalloc(&p, 4096));
+    HIP_TRY(hipMemset(p, 0, 4096));
+    z = reinterpret_cast<uint32_t*>(p);
+    d = reinterpret_cast<double*>(reinterpret_cast<char*>(p) + 256);
+  }
+  *zero32 = z;
+  *dump = d;
+  return FA_OK;
+}
+
 template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT, int VAR = 0>
 static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const GatherStage& W) {
   using R = Rec<GD, NV, NQ, MAT>;
@@ -4382,6 +4770,41 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   }
   P.rec = rec;
   P.bcmask = mask;
+  if constexpr (MAT == MAT_LINU && R::SIMP && NN % NSPLIT == 0 && NN * GD <= 32 && NN < 64) {
+    // the store-decoupled gather (k_gather_lin): positional plans of <= 256 items per chunk
+    if (P.nchunks > 0 && W.mode != GatherStage::PREP && !P.cw && lin_gather_enabled() && P.eadj && P.slots &&
+        P.slot_order == NSPLIT && !P.corder && P.plan_maxadj * NSPLIT <= 256 && P.plan_maxadj >= 0) {
+      if (P.plan_maxb > gather_maxb(false, GD * GD))
+        return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, the kernel %d", P.plan_maxb,
+                    gather_maxb(false, GD * GD));
+      if (P.nchunks >= (1ll << 31)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks", (long long)P.nchunks);
+      const double nu = P.F.nu, rr = 2.0 * nu / (1.0 - 2.0 * nu);
+      double* bhat = nullptr;
+      if ((rc = scratch_alloc((void**)&bhat, sizeof(double) * NN * NN * GD * GD, s))) return rc;
+      k_bhat<GD><<<grid_for(NN * NN), 256, 0, s>>>(P.ahat, NN * NN, rr, bhat);
+      LAUNCH_CHECK();
+      P.ahat = bhat;
+      P.trc = 1.0 / (1.0 + rr);
+      P.rlm = rr;
+      uint32_t* zero32 = nullptr;
+      double* dump = nullptr;
+      if ((rc = lin_scratch(&zero32, &dump))) return rc;
+      const int64_t grid = gather_grid(k_gather_lin<GD, NN, NSPLIT>, P.nchunks);
+      const int64_t per = (P.nchunks + grid - 1) / grid;
+      k_gather_lin<GD, NN, NSPLIT><<<(unsigned)grid, 256, 0, s>>>(P, zero32, dump, per);
+      LAUNCH_CHECK();
+      if (bc) {  // Dirichlet diagonals (dolfinx set_diagonal) of the plan's rows
+        k_bc_diag<GD><<<grid_for((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
+        LAUNCH_CHECK();
+      }
+      HIP_TRY(hipFreeAsync(bhat, s));
+      if (W.mode == GatherStage::FULL) {
+        HIP_TRY(hipFreeAsync(rec, s));
+        if (mask) HIP_TRY(hipFreeAsync(mask, s));
+      }
+      return FA_OK;
+    }
+  }
   if (P.nchunks > 0 && W.mode != GatherStage::PREP) {
     int64_t* desc = nullptr;
     if ((rc = chunk_desc(P, &desc, s))) return rc;
@@ -4637,7 +5060,7 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
       return fail(FA_E_ARG, "FA_GATHER needs the adjacency and a plan (fa_plan_gather)");
     GatherArgs P;
     P.M = M; P.F = F; P.A = Av;
-    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks; P.corder = plan->corder; P.plan_maxb = plan->max_blocks;
+    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks; P.corder = plan->corder; P.plan_maxb = plan->max_blocks; P.plan_maxadj = plan->max_adj;
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;
@@ -4716,7 +5139,7 @@ static int gather_stage(const fa_mesh* mesh, const fa_form* form, const fa_adjac
     if (!adj || !adj->ptr || !adj->idx || !plan || !plan->row_start)
       return fail(FA_E_ARG, "fa_gather_rows needs the adjacency and a plan (fa_plan_gather)");
     P.A = BsrView{A->indptr, A->indices, A->data, wb, we};
-    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks; P.corder = plan->corder; P.plan_maxb = plan->max_blocks;
+    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks; P.corder = plan->corder; P.plan_maxb = plan->max_blocks; P.plan_maxadj = plan->max_adj;
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;
@@ -4828,7 +5251,8 @@ __global__ __launch_bounds__(256) void k_vector(MeshView M, FormView F, DevTable
             if (F.d) dq += F.d[n];
           }
           double sig[2][2];
-          damage_stress(gr[0][0], gr[1][1], 0.5 * (gr[0][1] + gr[1][0]), lam, mu, dq * (1.0 / 3.0), w, sig);
+          if (F.ad) damage_stress_ad(gr[0][0], gr[1][1], 0.5 * (gr[0][1] + gr[1][0]), lam, mu, dq * (1.0 / 3.0), w, sig);
+          else damage_stress(gr[0][0], gr[1][1], 0.5 * (gr[0][1] + gr[1][0]), lam, mu, dq * (1.0 / 3.0), w, sig);
 #pragma unroll
           for (int i = 0; i < 2; ++i) r[i] += sig[i][0] * g[aloc][0] + sig[i][1] * g[aloc][1];
         } else {
@@ -5005,7 +5429,7 @@ __global__ __launch_bounds__(256) void k_lifting(MeshView M, FormView F, DevTabl
 #define FA_VEC_DISPATCH(KERNEL, ...)                                                              \
   do {                                                                                            \
     const int g_ = grid_for(mesh->nnodes);                                                        \
-    const bool dam_ = form->kind == FA_ASYM_DAMAGE;                                               \
+    const bool dam_ = F.kind == FA_ASYM_DAMAGE; /* FA_ASYM_DAMAGE_AD maps here, F.ad set */       \
     switch (mesh->cell_type) {                                                                    \
       case FA_TRIANGLE:                                                                           \
         if (dam_) KERNEL<2, 3, FA_ASYM_DAMAGE><<<g_, 256, 0, s>>>(__VA_ARGS__);                   \

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -377,7 +378,7 @@ def _combine_bcs(V: FunctionSpace, bcs, with_g: bool = True):
     cache = V.__dict__.setdefault("_bc_cache", {})
     key = _bcs_key(V, bcs, with_g)
     hit = cache.get(key)
-    if hit is not None:
+    if hit is not None and all(w() is bc for w, bc in zip(hit[2], bcs)):
         return hit[0], hit[1]
     marker = torch.zeros(V.num_dofs, dtype=torch.int8, device=V.mesh.device)
     g = torch.zeros(V.num_dofs, dtype=torch.float64, device=V.mesh.device) if with_g else None
@@ -387,7 +388,9 @@ def _combine_bcs(V: FunctionSpace, bcs, with_g: bool = True):
             g[bc.dofs] = bc.g[bc.dofs]
     if len(cache) >= 8:  # a handful of bcs sets per space; drop the oldest
         cache.pop(next(iter(cache)))
-    cache[key] = (marker, g, list(bcs))  # the bcs stay referenced: their ids cannot be reused
+    # weak references (a bc refers to V: strong ones would make a cycle that keeps V's tensors alive
+    # until a GC pass); a hit is checked against them, so a reused id of a dead bc cannot match
+    cache[key] = (marker, g, [weakref.ref(bc) for bc in bcs])
     return marker, g
 
 
@@ -424,9 +427,18 @@ class AsymDamage(LinearElasticity):
     u: displacement Function, d: damage (P1 scalar Function or per-node tensor)."""
     kind = _lib.FA_ASYM_DAMAGE
 
-    def __init__(self, V: FunctionSpace, E=None, nu=0.3, u=None, d=None, lam=None, mu=None, f=None):
+    def __init__(self, V: FunctionSpace, E=None, nu=0.3, u=None, d=None, lam=None, mu=None, f=None,
+                 tangent: str = "hand"):
+        """tangent: "hand" (the reference's default build: eigen-decomposition tangent and stress,
+        :207-329, :766-881) or "ad" (its USE_AD build: forward-over-forward AD of the damage
+        potential, :100-204, :752-763)."""
         super().__init__(V, E=E, nu=nu, lam=lam, mu=mu, quadrature_degree=1, u=u, f=f)
         self.d = None if d is None else (d.x if isinstance(d, Function) else d)
+        if tangent not in ("hand", "ad"):
+            raise ValueError(f"tangent must be 'hand' or 'ad', not {tangent!r}")
+        self.tangent = tangent
+        if tangent == "ad":
+            self.kind = _lib.FA_ASYM_DAMAGE_AD
 
 
 class NeoHookean(LinearElasticity):

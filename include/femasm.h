@@ -55,6 +55,9 @@ extern "C" {
 #define FA_LINEAR_ELASTICITY 0 /* sigma = lambda tr(eps) I + 2 mu eps  (reference J with d = 0) */
 #define FA_ASYM_DAMAGE 1       /* reference mechanic2d damage law, P1 triangles (2-D plane strain) */
 #define FA_NEO_HOOKEAN 2       /* compressible neo-Hookean, AD tangent */
+#define FA_ASYM_DAMAGE_AD 3    /* FA_ASYM_DAMAGE with the tangent and stress of the reference's USE_AD build:
+                                  forward-over-forward AD of its damage potential
+                                  (MFEM/mechanic2d/asym_elasto_damage_model.cc:100-204, :752-763) */
 
 /* fa_assemble_matrix flags */
 #define FA_GATHER 0x0        /* row-gather: each BSR row computed once, plain coalesced stores */

@@ -101,9 +101,11 @@ def test_owner_equals_lds_atomic_gather(oracle, dev, monkeypatch, ct, p, n):
     assert_rows_close(out["1"][0], out["0"][0], out["0"][1], 1e-13)
 
 
-def test_contrib_plan_refuses_oversized_chunks(oracle, dev):
-    """fa_plan_contrib checks the chunking: a default gather plan (up to 512 entries per chunk)
-    is refused with FA_E_CAPACITY rather than overrunning the kernel's cell staging."""
+def test_contrib_plan_refuses_oversized_chunks(oracle, dev, monkeypatch):
+    """fa_plan_contrib checks the chunking: a k_gather plan (up to 512 entries per chunk; with
+    FEMASM_LIN_GATHER=0, as simplex plans otherwise stop at k_gather_lin's 256 items) is refused
+    with FA_E_CAPACITY rather than overrunning the kernel's cell staging."""
+    monkeypatch.setenv("FEMASM_LIN_GATHER", "0")
     import ctypes
 
     from femasm import _lib, fem
