@@ -1774,6 +1774,10 @@ __device__ __forceinline__ void out_store(const T& v, T* p) {
 #ifndef FA_ABL
 #define FA_ABL 0
 #endif
+// timing-only ablations of the neo-Hookean gather items: 1 no per-point record loads, 2 no LDS adds
+#ifndef FA_NEO_ABL
+#define FA_NEO_ABL 0
+#endif
 #ifndef FA_GATHER_TIMING
 #define FA_GATHER_TIMING 0  // 1: per-phase shader-clock totals of the gather (measurement build)
 #endif
@@ -2023,7 +2027,7 @@ void k_gather(GatherArgs P) {
   // (neo-Hookean: measured 3 % faster without the permutation, n = 120)
   constexpr bool PERM = FA_GATHER_PERMUTE && !NEO;
   // kernels that can run a positional plan (the ordered-slot affine-simplex elasticity path)
-  constexpr bool POSM = (MAT == 0 || MAT == MAT_LINU || (MAT == MAT_AFFT && NN * GD <= 32)) && SIMP &&
+  constexpr bool POSM = (MAT == 0 || MAT == MAT_LINU || (MAT == MAT_AFFT && NN * GD <= 32) || NEO) && SIMP &&
                         NN % NSPLIT == 0;
   // barycentric blocks (bary_blocks): static column parts, one part per half (NSPLIT = 2) of the
   // workgroup so a wave's items share their code path; needs the plain (unordered) slot map
@@ -2216,6 +2220,21 @@ void k_gather(GatherArgs P) {
       constexpr int N = R::N;
       const double* Aq0 = P.rec + c * R::SIZE + R::QOFF;
       const double wdet = r[BS2];
+      // the item's columns: in the plan's bank-balanced order with their chunk-relative slots
+      // (positional plan: (b << 10) | position), else the cell's nodes of this part in order
+      int ocol[NBG], opos[NBG];
+      const bool ordered = posm && P.slot_order == NSPLIT;
+#pragma unroll
+      for (int bb = 0; bb < NBG; ++bb) {
+        if (ordered) {
+          const int v = (int)P.slots[(a0 + j) * NN + part * NBG + bb];
+          ocol[bb] = v >> 10;
+          opos[bb] = v & 1023;
+        } else {
+          ocol[bb] = min(part * NBG + bb, NN - 1);  // past-the-end columns: computed, never added
+          opos[bb] = -1;
+        }
+      }
       double K[NBG][GD][GD];
 #pragma unroll
       for (int bb = 0; bb < NBG; ++bb)
@@ -2230,18 +2249,25 @@ void k_gather(GatherArgs P) {
         const double* Q0 = P.rec + R::point0(c);
         constexpr int NL = R::SREC ? N + 1 : (FA_NEO_CREC ? N + 3 : N + 5);
         double Qn[NL];
+#if FA_NEO_ABL == 1
+#pragma unroll
+        for (int t = 0; t < NL; ++t) Qn[t] = 0.25 + 0.01 * t + 1e-12 * (double)c;
+#else
 #pragma unroll
         for (int t = 0; t < NL; ++t) Qn[t] = Q0[t];
+#endif
 #pragma unroll 1
         for (int q = 0; q < NQ; ++q) {
           double Qc[NL];
 #pragma unroll
           for (int t = 0; t < NL; ++t) Qc[t] = Qn[t];
+#if FA_NEO_ABL != 1
           {
             const double* Qx = Q0 + min(q + 1, NQ - 1) * R::PSTR;  // next point (the last one re-reads)
 #pragma unroll
             for (int t = 0; t < NL; ++t) Qn[t] = Qx[t];
           }
+#endif
           double ga[GD];
 #pragma unroll
           for (int d = 0; d < GD; ++d) {
@@ -2292,7 +2318,7 @@ void k_gather(GatherArgs P) {
           }
 #pragma unroll
           for (int bb = 0; bb < NBG; ++bb) {
-            const int b = min(part * NBG + bb, NN - 1);  // past-the-end columns: computed, never added
+            const int b = ocol[bb];
             double gb[GD], Cb[GD], dot = 0.0;
 #pragma unroll
             for (int d = 0; d < GD; ++d) {
@@ -2344,7 +2370,7 @@ void k_gather(GatherArgs P) {
         double gb[NBG][GD];  // column gradients of the item
 #pragma unroll
         for (int bb = 0; bb < NBG; ++bb) {
-          const int b = min(part * NBG + bb, NN - 1);  // past-the-end columns: computed, never added
+          const int b = ocol[bb];
 #pragma unroll
           for (int d = 0; d < GD; ++d) {
             double sgd = 0.0;
@@ -2405,12 +2431,17 @@ void k_gather(GatherArgs P) {
       }
 #pragma unroll
       for (int bb = 0; bb < NBG; ++bb) {
-        const int b = part * NBG + bb;
-        if (b >= NN) break;
-        int s = P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_slot(cols, lo, hi, cn[bb], niter);
+        if (part * NBG + bb >= NN) break;
+        const int b = ocol[bb];
+        int s = ordered ? opos[bb]
+                        : (P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_slot(cols, lo, hi, cn[bb], niter));
         bad |= s < 0;
         s = s < 0 ? MAXB : s;
+#if FA_NEO_ABL == 2
+        if (K[bb][0][0] == 1.2345e-300) acc[s * BS2] = K[bb][1][1];
+#else
         lds_add_block<GD>(acc, s, K[bb], (mask >> (aloc * GD)) & ((1u << GD) - 1), (mask >> (b * GD)) & ((1u << GD) - 1));
+#endif
       }
     } else if constexpr (SIMP) {
       if constexpr (BARY) {
@@ -2866,6 +2897,14 @@ void k_gather(GatherArgs P) {
 // be a conditional vector-memory operation), XCD-contiguous. Dirichlet diagonals are set after the
 // launch (k_bc_diag), items zero every constrained entry as in k_gather. Plans: <= 256 items per
 // chunk (fa_plan_gather caps a chunk at 256 / NSPLIT adjacency entries for these elements).
+#ifndef FA_LIN_NT
+#define FA_LIN_NT 1  // k_gather_lin chunk stores: 1 non-temporal, 0 plain
+#endif
+template <typename T>
+__device__ __forceinline__ void lin_store(const T& v, T* p) {
+  if constexpr (FA_LIN_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 #ifndef FA_LIN_ABL
 // timing-only ablations of k_gather_lin (wrong results; tools/lin_ablate.sh): 1 plain read-add-write
 // instead of LDS atomics (races), 2 no accumulator adds, 3 no table reads, 4 no chunk stores,
@@ -2889,10 +2928,17 @@ __global__ __launch_bounds__(256, 4) void k_gather_lin(GatherArgs P, const uint3
   __shared__ double tab[NN * NN * BS2];
   dv2* acc2 = reinterpret_cast<dv2*>(acc);
   const int tid = threadIdx.x;
+  // Chunk schedule: rounds of G consecutive chunks; in each round the 8 XCDs take 8 adjacent blocks
+  // of G / 8 chunks (blocks b and b + 8 share an XCD under round-robin dispatch; speed only). The
+  // chunks being written at any time then lie in one window of ~G chunks (the HBM write stream
+  // measured 6.0-7.0 TB/s when concurrent writes are close together, 5.3-5.5 TB/s when every
+  // workgroup streams its own distant range: tools/probe/hbm_probe.py), and the chunks
+  // that share cells run on one XCD at the same time (their records stay in its L2).
   const int G = gridDim.x;  // a multiple of 8
-  const int64_t wg = (int64_t)(blockIdx.x % 8) * (G / 8) + blockIdx.x / 8;
-  const int64_t c_begin = min(wg * per, P.nchunks), c_end = min(c_begin + per, P.nchunks);
-  if (c_begin >= c_end) return;  // the whole workgroup
+  const int64_t pos = (int64_t)(blockIdx.x % 8) * (G / 8) + blockIdx.x / 8;
+  const int64_t cnt = pos < P.nchunks ? (P.nchunks - pos + G - 1) / G : 0;  // this workgroup's chunks
+  if (cnt == 0) return;  // the whole workgroup
+  (void)per;
   for (int t = tid; t < NN * NN * BS2; t += 256) tab[t] = P.ahat[t];
   for (int t = tid; t < NP2; t += 256) acc2[t] = dv2{0.0, 0.0};
 
@@ -2902,8 +2948,8 @@ __global__ __launch_bounds__(256, 4) void k_gather_lin(GatherArgs P, const uint3
   const uint32_t* __restrict__ mk = P.bcmask ? P.bcmask : zero32;
   const uint32_t mkmul = P.bcmask ? 1u : 0u;
   struct Desc { int64_t b0, b1, a0, a1; };
-  auto desc = [&](int64_t c) -> Desc {  // clamped to the workgroup's last chunk: static loads
-    c = min(c, c_end - 1);
+  auto desc = [&](int64_t i) -> Desc {  // the workgroup's i-th chunk, clamped to its last: static loads
+    const int64_t c = pos + min(i, cnt - 1) * G;
     const int64_t r0 = sload(P.row_start, c), r1 = sload(P.row_start, c + 1);
     return Desc{sload(P.A.indptr, r0), sload(P.A.indptr, r1), sload(P.adj_ptr, r0), sload(P.adj_ptr, r1)};
   };
@@ -2943,7 +2989,7 @@ __global__ __launch_bounds__(256, 4) void k_gather_lin(GatherArgs P, const uint3
     it.mask = mk[c * mkmul] * mkmul;
   };
 
-  Desc d0 = desc(c_begin), d1 = desc(c_begin + 1), d2 = desc(c_begin + 2);
+  Desc d0 = desc(0), d1 = desc(1), d2 = desc(2);
   int32_t pf0 = load_entry(d0), pf1 = load_entry(d1);
   Item cur, nxt;
   load_item(d0, pf0, cur);
@@ -2952,7 +2998,7 @@ __global__ __launch_bounds__(256, 4) void k_gather_lin(GatherArgs P, const uint3
   // loop's waits are not widened by pending prologue loads merged in at the loop head)
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();  // table and accumulator staged
-  for (int64_t k = c_begin; k < c_end; ++k) {
+  for (int64_t k = 0; k < cnt; ++k) {
     // L1: chunk k+2's entry ids; L2: chunk k+1's records / slots / masks (before chunk k's stores)
     const int32_t pf2 = load_entry(d2);
     load_item(d1, pf1, nxt);
@@ -3079,9 +3125,9 @@ __global__ __launch_bounds__(256, 4) void k_gather_lin(GatherArgs P, const uint3
     if (hv == 1.2345e-300) out[0] = tv + v[0].x + v[SW - 1].y;
 #else
 #pragma unroll
-    for (int u = 0; u < SW; ++u) __builtin_nontemporal_store(v[u], out2 + max(min(tid + 256 * u, np - 1), 0));
-    __builtin_nontemporal_store(hv, out);
-    __builtin_nontemporal_store(tv, out + max(nv - 1, 0));
+    for (int u = 0; u < SW; ++u) lin_store(v[u], out2 + max(min(tid + 256 * u, np - 1), 0));
+    lin_store(hv, out);
+    lin_store(tv, out + max(nv - 1, 0));
 #endif
     __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics
     // rotate the pipeline
@@ -4473,12 +4519,17 @@ __global__ __launch_bounds__(256) void k_chunk_points(MeshView M, const int64_t*
   unsigned long long lmin[3] = {~0ull, ~0ull, ~0ull}, lmax[3] = {0ull, 0ull, 0ull};
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nchunks; k += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = adj_ptr[row_start[k]];
-    const int64_t c = adj_idx[e] / M.nn;
     double p[3] = {0.0, 0.0, 0.0};
-    for (int v = 0; v < M.nv; ++v)
-      for (int i = 0; i < M.gd; ++i) p[i] += M.x[(int64_t)M.geom[c * M.nv + v] * M.gd + i];
+    // a chunk whose rows touch no cell (unused nodes) has no entry to locate it: it keeps the
+    // origin as its point (any order assembles the same matrix)
+    const bool has = e < adj_ptr[row_start[k + 1]];
+    if (has) {
+      const int64_t c = adj_idx[e] / M.nn;
+      for (int v = 0; v < M.nv; ++v)
+        for (int i = 0; i < M.gd; ++i) p[i] += M.x[(int64_t)M.geom[c * M.nv + v] * M.gd + i];
+    }
     for (int i = 0; i < 3; ++i) {
-      p[i] /= (double)M.nv;
+      p[i] = has ? p[i] / (double)M.nv : 0.0;
       pts[k * 3 + i] = p[i];
       const unsigned long long q = ordered_key(p[i]);
       lmin[i] = min(lmin[i], q);
@@ -4719,16 +4770,16 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   using R = Rec<GD, NV, NQ, MAT>;
   // ordered (packed) slots are read only by the affine-simplex linear kernel of the same NSPLIT;
   // any other kernel searches its slots in LDS instead
-  if (P.slot_order && !((MAT == 0 || MAT == MAT_LINU || MAT == MAT_AFFT) && R::SIMP && NN % NSPLIT == 0 &&
-                        P.slot_order == NSPLIT)) {
+  if (P.slot_order && !((MAT == 0 || MAT == MAT_LINU || MAT == MAT_AFFT || MAT == FA_NEO_HOOKEAN) && R::SIMP &&
+                        NN % NSPLIT == 0 && P.slot_order == NSPLIT)) {
     P.slots = nullptr;
     P.slot_order = 0;
     P.eadj = nullptr;
   }
   // a positional plan's slot map is by position: a kernel without positional items (k_gather's
   // POSM) cannot read it -- search the slots in LDS instead
-  constexpr bool POSM_K = (MAT == 0 || MAT == MAT_LINU || (MAT == MAT_AFFT && NN * GD <= 32)) && R::SIMP &&
-                          NN % NSPLIT == 0;
+  constexpr bool POSM_K = (MAT == 0 || MAT == MAT_LINU || (MAT == MAT_AFFT && NN * GD <= 32) || MAT == FA_NEO_HOOKEAN) &&
+                          R::SIMP && NN % NSPLIT == 0;
   if (P.eadj && !POSM_K) {
     P.slots = nullptr;
     P.slot_order = 0;
@@ -4982,7 +5033,9 @@ static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const
   }
   if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, 0>(P, bc, s, W);
   if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, 0>(P, bc, s, W);
-  if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, 0>(P, bc, s, W);
+  // the column split of the plan's order (lin_simplex_nsplit): a P1-tet plan ordered for
+  // FA_P1TET_NSPLIT keeps its positional slot map with this kernel too
+  if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, FA_P1TET_NSPLIT, 0>(P, bc, s, W);
   if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, FA_P2TET_NSPLIT, 0>(P, bc, s, W);
   if (ct == FA_QUADRILATERAL && p == 1 && nq == 4) return launch_gather<2, 4, 4, 4, 1, 0>(P, bc, s, W);
   if (ct == FA_QUADRILATERAL && p == 2 && nq == 9) return launch_gather<2, 9, 4, 9, 3, 0>(P, bc, s, W);
@@ -5624,6 +5677,32 @@ __global__ __launch_bounds__(256) void k_hbm_write_span(double* __restrict__ dst
   }
 }
 
+// one-shot grids (one workgroup per contiguous piece, no grid-stride loop): each workgroup writes
+// PER consecutive KiB with 16 B per lane per instruction (LANE32: each lane 32 contiguous bytes)
+template <int PER, bool NT, bool LANE32>
+__global__ __launch_bounds__(256) void k_hbm_write_oneshot(double* __restrict__ dst, int64_t n2, double v) {
+  typedef double dv2 __attribute__((ext_vector_type(2)));
+  dv2* d2 = reinterpret_cast<dv2*>(dst);
+  const dv2 x = dv2{v, v};
+  const int64_t base = (int64_t)blockIdx.x * (PER * 64);  // dv2 per workgroup
+#pragma unroll
+  for (int u = 0; u < PER / 4; ++u) {
+    const int64_t i = LANE32 ? base + 2 * (int64_t)(u * 256 + threadIdx.x) / 2 * 1 + 0 : base + u * 256 + threadIdx.x;
+    if (LANE32) {
+      const int64_t j = base + (int64_t)(u * 256 + threadIdx.x) * 2;  // covers 2 * 256 dv2 per u: PER / 8 rounds
+      if (u < PER / 8) {
+        if (j + 1 < n2) {
+          if (NT) { __builtin_nontemporal_store(x, d2 + j); __builtin_nontemporal_store(x, d2 + j + 1); }
+          else { d2[j] = x; d2[j + 1] = x; }
+        }
+      }
+    } else if (i < n2) {
+      if (NT) __builtin_nontemporal_store(x, d2 + i);
+      else d2[i] = x;
+    }
+  }
+}
+
 extern "C" int fa_hbm_probe(int32_t mode, double* dst, const double* src, int64_t n, void* stream) {
   if (n <= 0 || (n & 1)) return fail(FA_E_ARG, "n must be positive and even");
   if (!dst || (mode != 1 && !src)) return fail(FA_E_ARG, "null argument");
@@ -5652,6 +5731,11 @@ extern "C" int fa_hbm_probe(int32_t mode, double* dst, const double* src, int64_
     case 17: k_hbm_write_span<1, false, false><<<grid, 256, 0, s>>>(dst, n / 2, 1.0); break;
     case 18: k_hbm_write_span<4, false, false><<<grid / 2, 256, 0, s>>>(dst, n / 2, 1.0); break;
     case 19: k_hbm_write_span<4, false, false><<<grid * 2, 256, 0, s>>>(dst, n / 2, 1.0); break;
+    case 20: k_hbm_write_oneshot<4, false, false><<<(unsigned)((n / 2 + 255) / 256), 256, 0, s>>>(dst, n / 2, 1.0); break;
+    case 21: k_hbm_write_oneshot<16, false, false><<<(unsigned)((n / 2 + 1023) / 1024), 256, 0, s>>>(dst, n / 2, 1.0); break;
+    case 22: k_hbm_write_oneshot<16, true, false><<<(unsigned)((n / 2 + 1023) / 1024), 256, 0, s>>>(dst, n / 2, 1.0); break;
+    case 23: k_hbm_write_oneshot<8, false, true><<<(unsigned)((n / 2 + 511) / 512), 256, 0, s>>>(dst, n / 2, 1.0); break;
+    case 24: k_hbm_write_oneshot<32, false, false><<<(unsigned)((n / 2 + 2047) / 2048), 256, 0, s>>>(dst, n / 2, 1.0); break;
     default: return fail(FA_E_ARG, "mode %d", mode);
   }
   LAUNCH_CHECK();

@@ -610,8 +610,9 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.
             slots = torch.empty(V.mesh.num_cells * V.nn * V.nn, dtype=torch.int16, device=V.mesh.device)
             _lib.check(L.fa_plan_slots(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), slots.data_ptr(),
                                        ctypes.byref(plan), sh), "fa_plan_slots")
-            if not neo:  # the ordered map serves the affine-simplex linear kernels only
-                eadj = _plan_order(V, fm, adj, fb, plan, sh)
+            # bank-balanced positional order of the LDS adds (affine-simplex elasticity and, with the
+            # same column split, the neo-Hookean gather)
+            eadj = _plan_order(V, fm, adj, fb, plan, sh)
         corder = _plan_locality(V, fm, adj, plan, sh)
         plans[key] = (plan, rs, A.indptr, slots, eadj, corder)
         V.__dict__.setdefault("_plan_xver", {})[key] = _coords_version(V.mesh)
@@ -725,8 +726,6 @@ class SplitGather:
             for i in live:
                 self.plans[i].slots = self.slots.data_ptr()
                 self.plans[i].slot_order = 0
-                if a.kind == _lib.FA_NEO_HOOKEAN:
-                    continue  # the neo-Hookean kernel reads the plain slot map
                 e = _plan_order(V, self.fm, self.adj, self.subs[i], self.plans[i], self.sh, self.eadj)
                 self.eadj = e if e is not None else self.eadj
 

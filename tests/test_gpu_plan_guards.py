@@ -1,0 +1,78 @@
+"""Plan-state guards (round 3): a plan is tied to the coordinates it was planned on, and plans of
+the store-decoupled affine-simplex gather (k_gather_lin) assemble the same matrix as k_gather."""
+import numpy as np
+import pytest
+import torch
+
+from rowparity import assert_rows_close
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+def _oracle_vals(oracle, V, a, marker=None):
+    m = V.mesh
+    cells = V.dofmap.cpu().numpy()
+    indptr, indices = oracle.sparsity(cells, V.num_nodes)
+    lam, mu = oracle.lame(a.E.cpu().numpy(), a.nu)
+    return oracle.assemble_elasticity(int(m.cell_type), V.degree, cells, m.cells.cpu().numpy(), m.x.cpu().numpy(),
+                                      lam, mu, indptr, indices, bc=None if marker is None else marker.cpu().numpy(),
+                                      diag=1.0, qdeg=a.qdeg)
+
+
+@pytest.mark.parametrize("ct,p,n", [(8, 2, (3, 2, 2)), (8, 3, (2, 2, 2)), (4, 2, (4, 3))])
+def test_vertices_moved_after_first_assembly(oracle, dev, ct, p, n):
+    """An affine tensor mesh is planned affine (the affine gather builds J from three edges); moving
+    its vertices in place afterwards must re-check the plan, not assemble the old geometry."""
+    from femasm import fem, mesh
+
+    m = mesh.create_unit_square(*n, cell_type=ct, device=dev) if len(n) == 2 else \
+        mesh.create_unit_cube(*n, cell_type=ct, device=dev)
+    V = fem.functionspace(m, ("Lagrange", p, (m.gdim,)))
+    E = torch.tensor(oracle.e_range()[np.arange(m.num_cells) % 200], device=dev)
+    a = fem.LinearElasticity(V, E=E, nu=0.3)
+    A = fem.assemble_matrix(a)
+    plan = fem.gather_plan(V, A, 0, a.kind)
+    assert plan.cell_flags & 1, "a structured box is affine"
+    assert_rows_close(A.data.cpu().numpy(), _oracle_vals(oracle, V, a), A.indptr.cpu().numpy(), RTOL)
+    # move interior vertices in place (mesh.x is a public tensor)
+    x = m.x
+    interior = ((x > 1e-9) & (x < 1 - 1e-9)).all(1)
+    g = torch.Generator().manual_seed(7)
+    x[interior] += (0.25 / max(n)) * (torch.rand(x[interior].shape, generator=g, dtype=torch.float64) - 0.5).to(dev)
+    A2 = fem.assemble_matrix(a, A=A)
+    assert not (fem.gather_plan(V, A, 0, a.kind).cell_flags & 1), "the moved mesh is no longer affine"
+    assert_rows_close(A2.data.cpu().numpy(), _oracle_vals(oracle, V, a), A2.indptr.cpu().numpy(), RTOL)
+
+
+@pytest.mark.parametrize("ct,p,n", [(-4, 2, (5, 4, 6)), (-4, 1, (7, 6, 5)), (3, 1, (13, 11)), (3, 2, (9, 8))])
+def test_lin_gather_equals_generic_gather(oracle, dev, monkeypatch, ct, p, n):
+    """k_gather_lin (default for uniform-nu affine simplices) and k_gather (FEMASM_LIN_GATHER=0) give
+    the same matrix, both equal to the oracle, with the reference bcs."""
+    from femasm import fem, mesh
+
+    monkeypatch.setenv("FEMASM_CONTRIB", "0")  # triangles: not the block-owner gather
+    out = []
+    for lin in ("1", "0"):
+        monkeypatch.setenv("FEMASM_LIN_GATHER", lin)
+        m = mesh.create_unit_square(*n, cell_type=ct, device=dev) if len(n) == 2 else \
+            mesh.create_unit_cube(*n, cell_type=ct, device=dev)
+        V = fem.functionspace(m, ("Lagrange", p, (m.gdim,)))
+        E = torch.tensor(oracle.e_range()[np.arange(m.num_cells) % 200], device=dev)
+        a = fem.LinearElasticity(V, E=E, nu=0.3)
+        left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
+        right = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.ones_like(x[0])))
+        bcs = [fem.dirichletbc(0.0, left, V), fem.dirichletbc([0.01] + [0.0] * (m.gdim - 1), right, V)]
+        A = fem.assemble_matrix(a, bcs=bcs)
+        marker, _ = fem._combine_bcs(V, bcs)
+        ref = _oracle_vals(oracle, V, a, marker)
+        assert_rows_close(A.data.cpu().numpy(), ref, A.indptr.cpu().numpy(), RTOL)
+        out.append(A.data.cpu().numpy())
+    assert_rows_close(out[0], out[1], A.indptr.cpu().numpy(), RTOL)

@@ -10,7 +10,9 @@ for gib in (4.0, 16.0):
     for mode, name, nb in ((0,"copy nt",16*n),(5,"copy plain",16*n),(1,"write nt",8*n),(3,"write plain",8*n),(6,"write nt 4x grid",8*n),(7,"write plain 4x grid",8*n),(2,"read nt",8*n),
                          (10,"span4 nt",8*n),(11,"span4 plain",8*n),(12,"span16 nt",8*n),(13,"span16 plain",8*n),
                          (14,"lane64 nt",8*n),(15,"lane64 plain",8*n),(16,"span1 nt",8*n),(17,"span1 plain",8*n),
-                         (18,"span4 plain half grid",8*n),(19,"span4 plain 2x grid",8*n)):
+                         (18,"span4 plain half grid",8*n),(19,"span4 plain 2x grid",8*n),
+                         (20,"oneshot 4KB/WG plain",8*n),(21,"oneshot 16KB/WG plain",8*n),(22,"oneshot 16KB/WG nt",8*n),
+                         (23,"oneshot 8KB/WG lane32",8*n),(24,"oneshot 32KB/WG plain",8*n)):
         L.fa_hbm_probe(mode, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(a.data_ptr()), n, sh)
         best = 1e9
         for _ in range(5):
