@@ -1504,6 +1504,17 @@ __global__ __launch_bounds__(256) void k_neo_records_tiled(MeshView M, FormView 
   }
 }
 
+// 16 zero bytes to LDS, the zero made at the store (volatile): hoisted out of the gather's chunk
+// loop, the compiler had kept the zero vector in scratch, and each reload waited vmcnt(0) -- for
+// every chunk store still in flight (stores count in vmcnt)
+__device__ __forceinline__ void lds_zero16(double* p) {
+  uint32_t a, b, c, d;
+  asm volatile("v_mov_b32 %0, 0\n\tv_mov_b32 %1, 0\n\tv_mov_b32 %2, 0\n\tv_mov_b32 %3, 0"
+               : "=v"(a), "=v"(b), "=v"(c), "=v"(d));
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  *reinterpret_cast<u4*>(p) = u4{a, b, c, d};
+}
+
 // Workgroup-uniform load through the scalar cache: a constant-address-space pointer lets the
 // compiler emit s_load (counted by lgkmcnt) instead of a vector load, whose vmcnt wait would also
 // drain every earlier vector load AND store of the wave (CDNA counts stores in vmcnt).
@@ -1893,6 +1904,7 @@ void k_gather(GatherArgs P) {
     qdone |= 1u << q;
   };
   auto grab = [&]() -> int64_t {
+#pragma unroll 1
     for (int t = 0; t < 9; ++t) {
       if (s_bat[0] < s_bat[1]) {
         const int64_t v = s_bat[0]++;
@@ -2013,9 +2025,8 @@ void k_gather(GatherArgs P) {
   };
   auto zero_acc = [&](const Desc& d) {  // after the barrier that follows the previous store
     const int nb_ = (int)(d.b1 - d.b0);
-    double2* acc2 = reinterpret_cast<double2*>(acc);
     const int nv2 = (nb_ * BS2 + 1) >> 1;  // acc holds (MAXB + 1) blocks: the odd tail fits
-    for (int t = tid; t < nv2; t += 256) acc2[t] = make_double2(0.0, 0.0);
+    for (int t = tid; t < nv2; t += 256) lds_zero16(acc + 2 * t);
   };
 
   // neo-Hookean items hold large per-q tangents: the prefetch registers would spill there
@@ -3010,7 +3021,10 @@ __global__ __launch_bounds__(256, 4) void k_gather_lin(GatherArgs P, const uint3
     const bool valid = jit < (int)(d0.a1 - d0.a0);
     {
       const int aloc = pf0 % NN;
-      const double* Ah0 = tab + aloc * NN * BS2;
+      // single ds_read_b64 per value (volatile: not merged into ds_read2_b64, which costs 8 LDS
+      // cycles per wave-instruction against 2 per ds_read_b64 for the same 16 bytes per lane)
+      typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
+      lds_vdouble* Ah0 = (lds_vdouble*)(tab + aloc * NN * BS2);
       const uint32_t rowm = (cur.mask >> (aloc * GD)) & ((1u << GD) - 1);
       const bool negw = __any(cur.r[BS2] < 0.0);  // wave-uniform: a cell with mu |J| < 0
       double Bn[BS2];
