@@ -3155,6 +3155,356 @@ __global__ __launch_bounds__(256, 4) void k_gather_lin(GatherArgs P, const uint3
   if (bad) atomicOr(P.err, 1);
 }
 
+// ------------------------------------------------------------------------------ neo-Hookean M gather
+// k_gather_neo: the neo-Hookean tangent (FA_NEO_HOOKEAN) on affine simplices with k_gather_lin's
+// store-decoupled schedule. With g_b = Ji^T dphi_b (dphi_b the reference gradient at point q) the
+// block is
+//   K_ab = sum_q [ s_c (M_q dphi_a)(M_q dphi_b)^T - rho_q (M_q dphi_b)(M_q dphi_a)^T ]
+//          + (sum_jl S_jl T_ab[j][l]) I,
+// M_q = sqrt(w_q |J|) C'_q Ji^T (C'_q = sqrt|c2| cof F_q, the scaled cofactor of FA_NEO_SREC),
+// S = mu |J| Ji Ji^T and T_ab[j][l] = sum_q w_q dphi_a[j] dphi_b[l] (the reference tensor of the
+// mu (g_a . g_b) I term, identical to the per-point sum: the same rule). Per block and point:
+// 3 LDS reads, V = M_q dphi_b (9 FMA), K += W V^T - V Z^T (18 FMA) with W = s_c M_q dphi_a and
+// Z = rho_q M_q dphi_a formed once per item; the mu term is 6 table reads and 6 FMA per block
+// (the per-point C g_b, g_b and dot of k_gather's neo items cost 42 FMA per block and point).
+// Records (NeoM, 64-cell tiles as FA_NEO_TILE): head S (upper triangle), s_c | per point M_q, rho_q.
+template <int GD, int NQ>
+struct NeoM {
+  static constexpr int NT = GD * (GD + 1) / 2;         // S / T entries: 00 11 (22) 01 (02 12)
+  static constexpr int HEAD = (NT + 1 + 1) & ~1;       // S, s_c (even)
+  static constexpr int PT = (GD * GD + 1 + 1) & ~1;    // M_q, rho_q (even)
+  static constexpr int SIZE = HEAD + NQ * PT;
+  __host__ __device__ static constexpr int64_t head(int64_t c) { return (c >> 6) * (64 * SIZE) + (c & 63) * HEAD; }
+  __host__ __device__ static constexpr int64_t point(int64_t c, int q) {
+    return (c >> 6) * (64 * SIZE) + 64 * HEAD + q * (64 * PT) + (c & 63) * PT;
+  }
+  __host__ __device__ static constexpr int64_t count(int64_t nc) { return (nc + 63) / 64 * 64 * SIZE; }
+};
+// symmetric-pair index of NeoM's S / T entries: (j, l) -> 0..NT-1 (diagonal first)
+template <int GD>
+__host__ __device__ constexpr int sym_pair(int j, int l) {
+  return j == l ? j : (GD == 2 ? 2 : (j + l == 1 ? 3 : (j + l == 2 ? 4 : 5)));
+}
+
+// NeoM records, one wave per 64-cell tile (lane = cell), each block of the tile staged in
+// wave-private LDS and stored as one contiguous run (as k_neo_records_tiled)
+template <int GD, int NN, int NQ>
+__global__ __launch_bounds__(256) void k_neo_records_m(MeshView M, FormView F, const double* __restrict__ tab,
+                                                       const int8_t* __restrict__ bc, double* __restrict__ rec,
+                                                       uint32_t* __restrict__ bcmask) {
+  using R = NeoM<GD, NQ>;
+  static_assert(NN * GD <= 32, "bc mask holds 32 dofs");
+  constexpr int N = GD * GD, HD = R::HEAD, PT = R::PT;
+  constexpr int BUF = 64 * (HD > PT ? HD : PT);
+  __shared__ __attribute__((aligned(16))) double sbuf[4][BUF];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* sb = sbuf[wave];
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  auto flush = [&](double* dst, int n) {  // sb[0, n) -> dst, n even, dst 16-B aligned
+    wave_sync();
+    const double2* s2 = reinterpret_cast<const double2*>(sb);
+    double2* d2 = reinterpret_cast<double2*>(dst);
+    for (int t = lane; t < n / 2; t += 64) d2[t] = s2[t];
+    wave_sync();
+  };
+  const int64_t ntiles = (M.ncells + 63) / 64;
+  for (int64_t tile = blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t c0 = tile * 64 + lane;
+    const bool valid = c0 < M.ncells;
+    const int64_t c = valid ? c0 : M.ncells - 1;  // lanes past the end fill the tile's padding
+    double* tb = rec + tile * (64 * R::SIZE);
+    double Ji[GD][GD];
+    const double det = fabs(simplex_geometry<GD>(M, c, Ji));
+    double lam, mu;
+    cell_lame(F, c, lam, mu);
+    const double sgn = lam > 0.0 ? 1.0 : (lam < 0.0 ? -1.0 : 0.0);  // sign of W_JJ + W_J/J = lam / J^2
+#pragma unroll
+    for (int j = 0; j < GD; ++j)
+#pragma unroll
+      for (int l = j; l < GD; ++l) {
+        double s = 0.0;
+#pragma unroll
+        for (int d = 0; d < GD; ++d) s = fma(Ji[j][d], Ji[l][d], s);
+        sb[lane * HD + sym_pair<GD>(j, l)] = mu * det * s;
+      }
+    sb[lane * HD + R::NT] = sgn;
+#pragma unroll
+    for (int t = R::NT + 1; t < HD; ++t) sb[lane * HD + t] = 0.0;
+    flush(tb, 64 * HD);
+    const int32_t* cn = M.cells + c * NN;
+    for (int q = 0; q < NQ; ++q) {
+      double Fq[N];
+      deformation_gradient<GD>(F.u, cn, NN, tab + NQ + q * NN * GD, Ji, Fq);
+      double I1 = GD == 2 ? 1.0 : 0.0, J;
+#pragma unroll
+      for (int m = 0; m < N; ++m) I1 = fma(Fq[m], Fq[m], I1);
+      if constexpr (GD == 2) J = Fq[0] * Fq[3] - Fq[1] * Fq[2];
+      else J = Fq[0] * (Fq[4] * Fq[8] - Fq[5] * Fq[7]) - Fq[1] * (Fq[3] * Fq[8] - Fq[5] * Fq[6]) +
+               Fq[2] * (Fq[3] * Fq[7] - Fq[4] * Fq[6]);
+      double co[5];
+      neo_energy_coeffs(I1, J, lam, mu, co);
+      double Cm[GD][GD];
+      cofactor<GD>(Fq, Cm);
+      const double a2 = fabs(co[2]);
+      const double sc = (sgn != 0.0 ? sqrt(a2) : 1.0) * sqrt(tab[q] * det);
+      const double rho = sgn != 0.0 ? co[3] / a2 : co[3];
+#pragma unroll
+      for (int i = 0; i < GD; ++i)
+#pragma unroll
+        for (int k = 0; k < GD; ++k) {
+          double m = 0.0;
+#pragma unroll
+          for (int d = 0; d < GD; ++d) m = fma(Cm[i][d], Ji[k][d], m);
+          sb[lane * PT + i * GD + k] = sc * m;
+        }
+      sb[lane * PT + N] = rho;
+#pragma unroll
+      for (int t = N + 1; t < PT; ++t) sb[lane * PT + t] = 0.0;
+      flush(tb + 64 * HD + q * (64 * PT), 64 * PT);
+    }
+    if (bcmask && valid) {
+      uint32_t m = 0;
+#pragma unroll
+      for (int b = 0; b < NN; ++b) {
+        const int64_t n = cn[b];
+#pragma unroll
+        for (int j = 0; j < GD; ++j) m |= (bc[n * GD + j] ? 1u : 0u) << (b * GD + j);
+      }
+      bcmask[c] = m;
+    }
+  }
+}
+
+#ifndef FA_NEOM_WAVES
+#define FA_NEOM_WAVES 2
+#endif
+// timing-only ablations of k_gather_neo (wrong results): 2 no accumulator adds, 4 no chunk stores
+#ifndef FA_NEOM_ABL
+#define FA_NEOM_ABL 0
+#endif
+template <int GD, int NN, int NQ, int NSPLIT>
+__global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P, const uint32_t* __restrict__ zero32,
+                                                                  double* __restrict__ dump) {
+  using R = NeoM<GD, NQ>;
+  constexpr int BS2 = GD * GD, NT = R::NT;
+  constexpr int NBG = NN / NSPLIT;
+  constexpr int MAXB = gather_maxb(true, BS2);
+  constexpr int NACC = MAXB * BS2 + 2;
+  constexpr int NP2 = (NACC + 1) / 2;
+  constexpr int SW = (MAXB * BS2 / 2 + 255) / 256;
+  static_assert(NN % NSPLIT == 0 && NN * GD <= 32 && NN <= 63 && MAXB < 1024, "k_gather_neo: affine simplices");
+  typedef double dv2 __attribute__((ext_vector_type(2)));
+  __shared__ __attribute__((aligned(16))) double acc[2 * NP2];
+  __shared__ double s_phi[NN * NQ * GD];  // [b][q][k]: a column's gradients at every point, contiguous
+  __shared__ double s_T[NN * NN * NT];    // [a][b][t]
+  dv2* acc2 = reinterpret_cast<dv2*>(acc);
+  const int tid = threadIdx.x;
+  // chunk schedule of k_gather_lin (round-interleaved XCD blocks); a locality order maps through corder
+  const int G = gridDim.x;
+  const int64_t pos = (int64_t)(blockIdx.x % 8) * (G / 8) + blockIdx.x / 8;
+  const int64_t cnt = pos < P.nchunks ? (P.nchunks - pos + G - 1) / G : 0;
+  if (cnt == 0) return;
+  const double* wq = P.tab;
+  const double* dphi = P.tab + NQ;  // [q][b][k]
+  for (int t = tid; t < NN * NQ * GD; t += 256) {
+    const int b = t / (NQ * GD), q = (t / GD) % NQ, k = t % GD;
+    s_phi[t] = dphi[(q * NN + b) * GD + k];
+  }
+  for (int t = tid; t < NN * NN; t += 256) {
+    const int a = t / NN, b = t % NN;
+    double Ah[GD][GD];
+#pragma unroll
+    for (int j = 0; j < GD; ++j)
+#pragma unroll
+      for (int l = 0; l < GD; ++l) Ah[j][l] = 0.0;
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int j = 0; j < GD; ++j)
+#pragma unroll
+        for (int l = 0; l < GD; ++l) Ah[j][l] = fma(wq[q] * dphi[(q * NN + a) * GD + j], dphi[(q * NN + b) * GD + l], Ah[j][l]);
+#pragma unroll
+    for (int j = 0; j < GD; ++j)
+#pragma unroll
+      for (int l = j; l < GD; ++l) s_T[t * NT + sym_pair<GD>(j, l)] = j == l ? Ah[j][j] : Ah[j][l] + Ah[l][j];
+  }
+  for (int t = tid; t < NP2; t += 256) acc2[t] = dv2{0.0, 0.0};
+
+  const int64_t abase = sload(P.A.indptr, P.A.row_begin);
+  const int64_t nent = P.M.ncells * NN;
+  const int32_t* __restrict__ eadj = P.eadj;
+  const uint32_t* __restrict__ mk = P.bcmask ? P.bcmask : zero32;
+  const uint32_t mkmul = P.bcmask ? 1u : 0u;
+  struct Desc { int64_t b0, b1, a0, a1; };
+  auto desc = [&](int64_t i) -> Desc {  // the workgroup's i-th chunk, clamped to its last: static loads
+    int64_t c = pos + min(i, cnt - 1) * G;
+    if (P.corder) c = sload(P.corder, c);
+    const int64_t r0 = sload(P.row_start, c), r1 = sload(P.row_start, c + 1);
+    return Desc{sload(P.A.indptr, r0), sload(P.A.indptr, r1), sload(P.adj_ptr, r0), sload(P.adj_ptr, r1)};
+  };
+  const int jit = tid / NSPLIT, part = tid % NSPLIT;
+  auto entry_of = [&](const Desc& d) -> int64_t {
+    const int na = (int)(d.a1 - d.a0);
+    int64_t e = d.a0 + min(jit, max(na - 1, 0));
+    return min(max(e, (int64_t)0), nent - 1);
+  };
+  auto load_entry = [&](const Desc& d) -> int32_t { return eadj[entry_of(d)]; };
+  struct Item { double hd[R::HEAD]; double pt[NQ][R::PT]; uint32_t sl[NBG]; uint32_t mask; };
+  auto load_item = [&](const Desc& d, int32_t pflat, Item& it) {
+    const int64_t c = pflat / NN;
+    const dv2* hp = reinterpret_cast<const dv2*>(P.rec + R::head(c));
+#pragma unroll
+    for (int k = 0; k < R::HEAD / 2; ++k) {
+      const dv2 v = hp[k];
+      it.hd[2 * k] = v.x;
+      it.hd[2 * k + 1] = v.y;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const dv2* pp = reinterpret_cast<const dv2*>(P.rec + R::point(c, q));
+#pragma unroll
+      for (int k = 0; k < R::PT / 2; ++k) {
+        const dv2 v = pp[k];
+        it.pt[q][2 * k] = v.x;
+        it.pt[q][2 * k + 1] = v.y;
+      }
+    }
+    const uint16_t* sp = P.slots + entry_of(d) * NN + part * NBG;
+#pragma unroll
+    for (int bb = 0; bb < NBG; ++bb) it.sl[bb] = sp[bb];
+    it.mask = mk[c * mkmul] * mkmul;
+  };
+
+  Desc d0 = desc(0), d1 = desc(1), d2 = desc(2);
+  int32_t pf0 = load_entry(d0), pf1 = load_entry(d1);
+  Item cur;
+  load_item(d0, pf0, cur);
+  int bad = 0;
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the prologue's loads (see k_gather_lin)
+  __syncthreads();                     // tables and accumulator staged
+  typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
+  for (int64_t k = 0; k < cnt; ++k) {
+    const int32_t pf2 = load_entry(d2);  // chunk k+2's entry ids
+    const Desc d3 = desc(k + 3);
+    const int64_t off = (d0.b0 - abase) * BS2;
+    const int h = (int)(off & 1);
+    const int nb = (int)(d0.b1 - d0.b0);
+    const bool valid = jit < (int)(d0.a1 - d0.a0);
+    {
+      const int aloc = pf0 % NN;
+      const uint32_t rowm = (cur.mask >> (aloc * GD)) & ((1u << GD) - 1);
+      const double sc = cur.hd[NT];
+      // per point: U = M_q dphi_a, W = s_c U, Z = rho_q U
+      double W[NQ][GD], Z[NQ][GD];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        double pa[GD];
+#pragma unroll
+        for (int kk = 0; kk < GD; ++kk) pa[kk] = s_phi[(aloc * NQ + q) * GD + kk];
+#pragma unroll
+        for (int i = 0; i < GD; ++i) {
+          double u = cur.pt[q][i * GD] * pa[0];
+#pragma unroll
+          for (int kk = 1; kk < GD; ++kk) u = fma(cur.pt[q][i * GD + kk], pa[kk], u);
+          W[q][i] = sc * u;
+          Z[q][i] = cur.pt[q][BS2] * u;
+        }
+      }
+      lds_vdouble* Ta = (lds_vdouble*)(s_T + aloc * NN * NT);
+#pragma unroll
+      for (int bb = 0; bb < NBG; ++bb) {
+        const int s = (int)(cur.sl[bb] & 1023u);
+        const int b = (int)(cur.sl[bb] >> 10);
+        lds_vdouble* pb = (lds_vdouble*)(s_phi + b * NQ * GD);
+        double K[GD][GD];
+#pragma unroll
+        for (int i = 0; i < GD; ++i)
+#pragma unroll
+          for (int kk = 0; kk < GD; ++kk) K[i][kk] = 0.0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          double pbq[GD], V[GD];
+#pragma unroll
+          for (int kk = 0; kk < GD; ++kk) pbq[kk] = pb[q * GD + kk];
+#pragma unroll
+          for (int i = 0; i < GD; ++i) {
+            double v = cur.pt[q][i * GD] * pbq[0];
+#pragma unroll
+            for (int kk = 1; kk < GD; ++kk) v = fma(cur.pt[q][i * GD + kk], pbq[kk], v);
+            V[i] = v;
+          }
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int kk = 0; kk < GD; ++kk) K[i][kk] = fma(W[q][i], V[kk], fma(-V[i], Z[q][kk], K[i][kk]));
+        }
+        double dot = 0.0;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) dot = fma(cur.hd[t], Ta[b * NT + t], dot);
+#pragma unroll
+        for (int i = 0; i < GD; ++i) K[i][i] += dot;
+        const uint32_t colm = (cur.mask >> (b * GD)) & ((1u << GD) - 1);
+        if (__any((rowm | colm) != 0u)) {
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int kk = 0; kk < GD; ++kk)
+              if (((rowm >> i) | (colm >> kk)) & 1u) K[i][kk] = 0.0;
+        }
+        bad |= valid && s >= nb;
+        if (valid && s < nb) {
+          double* ap = acc + h + s * BS2;
+#if FA_NEOM_ABL == 2
+          if (K[0][0] == 1.2345e-300) ap[0] = K[1][1];
+#else
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int kk = 0; kk < GD; ++kk) atomicAdd(ap + i * GD + kk, K[i][kk]);
+#endif
+        }
+      }
+    }
+    // chunk k+1's records / slots / masks: the item registers are dead here, and these loads are
+    // issued before chunk k's stores (their wait at chunk k+1 does not include the stores)
+    load_item(d1, pf1, cur);
+    __syncthreads();  // B1: the chunk is accumulated
+    const int nv = nb * BS2;
+    const int np = (nv - h) >> 1;
+    dv2 v[SW];
+#pragma unroll
+    for (int u = 0; u < SW; ++u) v[u] = acc2[h + max(min(tid + 256 * u, np - 1), 0)];
+    const double hv = acc[h], tv = acc[max(nv - 1, 0) + h];
+    __syncthreads();  // B2: every read is done before any zero
+#pragma unroll
+    for (int u = 0; u < SW; ++u)
+      if (tid + 256 * u < np) acc2[h + tid + 256 * u] = dv2{0.0, 0.0};
+    if (tid == 0) acc2[0] = dv2{0.0, 0.0};
+    if (tid == 1) acc2[(max(nv - 1, 0) + h) >> 1] = dv2{0.0, 0.0};
+    const bool none = np < 1;
+    double* out = none ? dump : P.A.data + off;
+    dv2* out2 = reinterpret_cast<dv2*>(none ? dump : out + h);
+#if FA_NEOM_ABL == 4
+    if (hv == 1.2345e-300) out[0] = tv + v[0].x + v[SW - 1].y;
+#else
+#pragma unroll
+    for (int u = 0; u < SW; ++u) lin_store(v[u], out2 + max(min(tid + 256 * u, np - 1), 0));
+    lin_store(hv, out);
+    lin_store(tv, out + max(nv - 1, 0));
+#endif
+    __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics
+    d0 = d1;
+    d1 = d2;
+    d2 = d3;
+    pf0 = pf1;
+    pf1 = pf2;
+  }
+  if (bad) atomicOr(P.err, 1);
+}
+
 // ------------------------------------------------------------------------------ block-owner gather
 // k_gather_own: the uniform-nu affine-simplex gather (MAT_LINU) without per-contribution LDS
 // atomics. The contribution plan (fa_plan_contrib) lists, per chunk, every (cell, row node a,
@@ -4779,6 +5129,67 @@ static int lin_scratch(uint32_t** zero32, double** dump) {
   return FA_OK;
 }
 
+// FEMASM_NEO_M=0: neo-Hookean simplices run k_gather's neo items (tiled C records) instead of k_gather_neo
+static bool neo_m_enabled() {
+  const char* e = getenv("FEMASM_NEO_M");
+  return !(e && e[0] == '0');
+}
+
+template <int GD, int NN, int NQ, int NSPLIT>
+static int launch_gather_neo(GatherArgs P, const int8_t* bc, hipStream_t s, const GatherStage& W) {
+  using R = NeoM<GD, NQ>;
+  const int64_t nc = P.M.ncells;
+  const int64_t rec_bytes = align256((int64_t)sizeof(double) * R::count(nc));
+  if (W.mode == GatherStage::SIZE) {
+    *W.bytes = rec_bytes + align256((int64_t)sizeof(uint32_t) * nc);
+    return FA_OK;
+  }
+  const bool rows = P.nchunks > 0 && W.mode != GatherStage::PREP;
+  if (rows) {  // the kernel's plan: positional, ordered for NSPLIT, <= 256 items per chunk
+    if (!(P.eadj && P.slots && P.slot_order == NSPLIT && !P.cw && P.plan_maxadj >= 0 && P.plan_maxadj * NSPLIT <= 256))
+      return fail(FA_E_ARG, "the neo-Hookean gather needs a positional plan ordered for %d column parts with <= %d "
+                  "entries per chunk (fa_plan_gather_form + fa_plan_slots + fa_plan_order), or FEMASM_NEO_M=0",
+                  NSPLIT, 256 / NSPLIT);
+    if (P.plan_maxb > gather_maxb(true, GD * GD))
+      return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, the kernel %d: plan with fa_plan_gather_form",
+                  P.plan_maxb, gather_maxb(true, GD * GD));
+    if (P.nchunks >= (1ll << 31)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks", (long long)P.nchunks);
+  }
+  double* rec = nullptr;
+  uint32_t* mask = nullptr;
+  int rc;
+  if (W.mode == GatherStage::FULL) {
+    if ((rc = scratch_alloc((void**)&rec, sizeof(double) * R::count(nc), s))) return rc;
+    if (bc && (rc = scratch_alloc((void**)&mask, sizeof(uint32_t) * nc, s))) return rc;
+  } else {
+    rec = reinterpret_cast<double*>(W.work);
+    mask = bc ? reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.work) + rec_bytes) : nullptr;
+  }
+  if (nc > 0 && W.mode != GatherStage::ROWS) {
+    k_neo_records_m<GD, NN, NQ><<<grid_for((nc + 63) / 64 * 64), 256, 0, s>>>(P.M, P.F, P.tab, bc, rec, mask);
+    LAUNCH_CHECK();
+  }
+  P.rec = rec;
+  P.bcmask = mask;
+  if (rows) {
+    uint32_t* zero32 = nullptr;
+    double* dump = nullptr;
+    if ((rc = lin_scratch(&zero32, &dump))) return rc;
+    const int64_t grid = gather_grid(k_gather_neo<GD, NN, NQ, NSPLIT>, P.nchunks);
+    k_gather_neo<GD, NN, NQ, NSPLIT><<<(unsigned)grid, 256, 0, s>>>(P, zero32, dump);
+    LAUNCH_CHECK();
+    if (bc) {  // Dirichlet diagonals (dolfinx set_diagonal) of the plan's rows
+      k_bc_diag<GD><<<grid_for((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
+      LAUNCH_CHECK();
+    }
+  }
+  if (W.mode == GatherStage::FULL) {
+    HIP_TRY(hipFreeAsync(rec, s));
+    if (mask) HIP_TRY(hipFreeAsync(mask, s));
+  }
+  return FA_OK;
+}
+
 template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT, int VAR = 0>
 static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const GatherStage& W) {
   using R = Rec<GD, NV, NQ, MAT>;
@@ -4809,6 +5220,11 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   {
     const char* e = getenv("FEMASM_CHUNK_ORDER_ALL");
     if (MAT != FA_NEO_HOOKEAN && !(e && e[0] == '1')) P.corder = nullptr;
+  }
+  if constexpr (MAT == FA_NEO_HOOKEAN && R::SIMP && NN % NSPLIT == 0 && NN * GD <= 32 && NN < 64) {
+    // the neo-Hookean M gather (k_gather_neo) and its records: chosen per process (FEMASM_NEO_M=0
+    // keeps k_gather's neo items), since the prepare stage of the split ABI has no plan
+    if (neo_m_enabled()) return launch_gather_neo<GD, NN, NQ, NSPLIT>(P, bc, s, W);
   }
   const int64_t nc = P.M.ncells;
   const int64_t rec_bytes = align256((int64_t)sizeof(double) * R::count(nc));
@@ -5032,7 +5448,8 @@ static int dispatch_gather(const fa_mesh* m, const DevTables& T, int kind, const
   if (kind == FA_ASYM_DAMAGE) return launch_gather<2, 3, 3, 1, 1, FA_ASYM_DAMAGE>(P, bc, s, W);
   if (kind == FA_NEO_HOOKEAN) {
     if (ct == FA_TETRAHEDRON && p == 2 && nq == 4) return launch_gather<3, 10, 4, 4, FA_NEO_NSPLIT, FA_NEO_HOOKEAN>(P, bc, s, W);
-    if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, 2, FA_NEO_HOOKEAN>(P, bc, s, W);
+    // P1 tets: the column split of the plan's order (lin_simplex_nsplit), so the positional slot map fits
+    if (ct == FA_TETRAHEDRON && p == 1 && nq == 1) return launch_gather<3, 4, 4, 1, FA_P1TET_NSPLIT, FA_NEO_HOOKEAN>(P, bc, s, W);
     if (ct == FA_TRIANGLE && p == 2 && nq == 3) return launch_gather<2, 6, 3, 3, 2, FA_NEO_HOOKEAN>(P, bc, s, W);
     if (ct == FA_TRIANGLE && p == 1 && nq == 1) return launch_gather<2, 3, 3, 1, 1, FA_NEO_HOOKEAN>(P, bc, s, W);
     *handled = false;
