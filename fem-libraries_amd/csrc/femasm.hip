@@ -1067,7 +1067,7 @@ __global__ void k_bc_diag(BsrView A, int64_t nnodes, const int8_t* __restrict__ 
 //     read one record + the column node ids, build 3x3 blocks in registers and add them into
 //     the LDS copy of the chunk; the chunk is then stored with coalesced plain stores.
 #ifndef FA_GATHER_LDS
-#define FA_GATHER_LDS 28672
+#define FA_GATHER_LDS 32768  // 4 workgroups / CU with k_gather_lin's table (E: 44.3 vs 45.3 ms at 28672)
 #endif
 static constexpr int kGatherLdsValues = FA_GATHER_LDS;  // accumulator bytes per workgroup (4 WG / CU)
 // neo-Hookean gather (2 workgroups / CU, VGPR-bound): a larger accumulator, and chunks capped at
@@ -2916,14 +2916,63 @@ __device__ __forceinline__ void lin_store(const T& v, T* p) {
   if constexpr (FA_LIN_NT) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
+
+// chunk drain without the read / zero barrier (chunk_drain): 1, or the two-barrier read-all /
+// zero-all drain: 0. k_gather_lin keeps the two-barrier drain: at its 128-VGPR cap chunk_drain's
+// buffer descriptor and pair registers spill uniform pointers whose reloads wait vmcnt(0) in the
+// item loop, i.e. for every chunk store in flight
+#ifndef FA_DRAIN_LIN
+#define FA_DRAIN_LIN 0
+#endif
+#ifndef FA_DRAIN_NEO
+#define FA_DRAIN_NEO 1
+#endif
+// Stream a chunk's nv accumulated values acc[h, h + nv) to out[0, nv) and leave the accumulator
+// zero, after the items barrier. The values form 16-B pairs acc2[j], j < j1 = (h + nv + 1) / 2; pair
+// j lands at out - h + 2j, 16-B aligned (out - h is). A lane reads, zeroes and stores its own pairs
+// (SW per lane, j = tid + 256 u), so no barrier separates the reads from the zeroes; the partial
+// pairs at the ends (head half when h = 1, tail half when h + nv is odd) are stored as single
+// values by their owners. Every lane issues exactly SW + 2 stores (lanes without a pair or a half
+// store to the scratch line `dump`): a static vector-memory count (see k_gather_lin).
+template <int SW, int NT = 256>
+__device__ __forceinline__ void chunk_drain(double* acc, int h, int nv, double* out, double* dump, int tid) {
+  typedef double dv2 __attribute__((ext_vector_type(2)));
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  typedef unsigned v2u __attribute__((ext_vector_type(2)));
+  (void)dump;
+  dv2* acc2 = reinterpret_cast<dv2*>(acc);
+  const int j1 = (h + nv + 1) >> 1;
+  const int jt = (h + nv - 1) >> 1;             // the pair holding the last value
+  const bool tail_half = ((h + nv) & 1) != 0;  // ... alone
+  // buffer stores over the chunk's 16-B-aligned span [out - h, out + nv): an offset past it is
+  // dropped by the range check (no traffic), so every lane issues the same stores
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out - h, 0, (h + nv) * 8, 0x00020000);
+  constexpr int OOB = 0x40000000;
+  constexpr int AUX = FA_LIN_NT ? 2 : 0;  // nt
+  double hv = 0.0, tv = 0.0;
+#pragma unroll
+  for (int u = 0; u < SW; ++u) {
+    const int j = tid + NT * u;
+    const int jj = max(min(j, j1 - 1), 0);
+    const dv2 v = acc2[jj];
+    if (j < j1) acc2[jj] = dv2{0.0, 0.0};
+    if (j == 0) hv = v.y;
+    if (j == jt) tv = v.x;
+    const bool full = j < j1 && !(j == 0 && h) && !(j == jt && tail_half);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), rs, full ? 16 * j : OOB, 0, AUX);
+  }
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, hv), rs, (tid == 0 && h) ? 8 : OOB, 0, AUX);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rs,
+                                        (tid == (jt % NT) && tail_half && !(jt == 0 && h)) ? 8 * (h + nv - 1) : OOB, 0, AUX);
+}
 #ifndef FA_LIN_ABL
 // timing-only ablations of k_gather_lin (wrong results; tools/lin_ablate.sh): 1 plain read-add-write
 // instead of LDS atomics (races), 2 no accumulator adds, 3 no table reads, 4 no chunk stores,
 // 5 no item loads (constant records / slots)
 #define FA_LIN_ABL 0
 #endif
-template <int GD, int NN, int NSPLIT>
-__global__ __launch_bounds__(256, 4) void k_gather_lin(GatherArgs P, const uint32_t* __restrict__ zero32,
+template <int GD, int NN, int NSPLIT, int NT = 256>
+__global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32_t* __restrict__ zero32,
                                                         double* __restrict__ dump, int64_t per) {
   using R = Rec<GD, GD + 1, 1, MAT_LINU>;
   constexpr int BS2 = GD * GD;
@@ -2931,7 +2980,7 @@ __global__ __launch_bounds__(256, 4) void k_gather_lin(GatherArgs P, const uint3
   constexpr int MAXB = gather_maxb(false, BS2);
   constexpr int NACC = MAXB * BS2 + 2;       // value p of a chunk at acc[p + h], h = its parity
   constexpr int NP2 = (NACC + 1) / 2;        // 16-B pairs of the accumulator
-  constexpr int SW = (MAXB * BS2 / 2 + 255) / 256;  // pair stores per lane per chunk
+  constexpr int SW = (MAXB * BS2 / 2 + NT - 1) / NT;  // pair stores per lane per chunk
   constexpr int RL = R::SIZE;
   static_assert(NN % NSPLIT == 0 && NN * GD <= 32 && RL % 2 == 0 && NN <= 63, "k_gather_lin: affine simplices");
   typedef double dv2 __attribute__((ext_vector_type(2)));
@@ -2950,8 +2999,8 @@ __global__ __launch_bounds__(256, 4) void k_gather_lin(GatherArgs P, const uint3
   const int64_t cnt = pos < P.nchunks ? (P.nchunks - pos + G - 1) / G : 0;  // this workgroup's chunks
   if (cnt == 0) return;  // the whole workgroup
   (void)per;
-  for (int t = tid; t < NN * NN * BS2; t += 256) tab[t] = P.ahat[t];
-  for (int t = tid; t < NP2; t += 256) acc2[t] = dv2{0.0, 0.0};
+  for (int t = tid; t < NN * NN * BS2; t += NT) tab[t] = P.ahat[t];
+  for (int t = tid; t < NP2; t += NT) acc2[t] = dv2{0.0, 0.0};
 
   const int64_t abase = sload(P.A.indptr, P.A.row_begin);
   const int64_t nent = P.M.ncells * NN;
@@ -3114,18 +3163,21 @@ __global__ __launch_bounds__(256, 4) void k_gather_lin(GatherArgs P, const uint3
       }
     }
     __syncthreads();  // B1: the chunk is accumulated
+    if constexpr (FA_DRAIN_LIN && FA_LIN_ABL != 4) {
+      chunk_drain<SW, NT>(acc, h, nb * BS2, P.A.data + off, dump, tid);
+    } else {
     // read the chunk into registers: pairs t (value 2t + h .. 2t + 1 + h at acc2[t + h]); lanes past
     // the chunk's pairs repeat the last pair, and every lane reads the unpaired head / tail value
     const int nv = nb * BS2;
     const int np = (nv - h) >> 1;
     dv2 v[SW];
 #pragma unroll
-    for (int u = 0; u < SW; ++u) v[u] = acc2[h + max(min(tid + 256 * u, np - 1), 0)];
+    for (int u = 0; u < SW; ++u) v[u] = acc2[h + max(min(tid + NT * u, np - 1), 0)];
     const double hv = acc[h], tv = acc[max(nv - 1, 0) + h];
     __syncthreads();  // B2: every read is done before any zero
 #pragma unroll
     for (int u = 0; u < SW; ++u)
-      if (tid + 256 * u < np) acc2[h + tid + 256 * u] = dv2{0.0, 0.0};
+      if (tid + NT * u < np) acc2[h + tid + NT * u] = dv2{0.0, 0.0};
     // the unpaired head (acc[1] when h = 1) and tail sit in pairs whose other half is never written
     if (tid == 0) acc2[0] = dv2{0.0, 0.0};
     if (tid == 1) acc2[(max(nv - 1, 0) + h) >> 1] = dv2{0.0, 0.0};
@@ -3139,10 +3191,11 @@ __global__ __launch_bounds__(256, 4) void k_gather_lin(GatherArgs P, const uint3
     if (hv == 1.2345e-300) out[0] = tv + v[0].x + v[SW - 1].y;
 #else
 #pragma unroll
-    for (int u = 0; u < SW; ++u) lin_store(v[u], out2 + max(min(tid + 256 * u, np - 1), 0));
+    for (int u = 0; u < SW; ++u) lin_store(v[u], out2 + max(min(tid + NT * u, np - 1), 0));
     lin_store(hv, out);
     lin_store(tv, out + max(nv - 1, 0));
 #endif
+    }
     __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics
     // rotate the pipeline
     d0 = d1;
@@ -3236,9 +3289,37 @@ __global__ __launch_bounds__(256) void k_neo_records_m(MeshView M, FormView F, c
     for (int t = R::NT + 1; t < HD; ++t) sb[lane * HD + t] = 0.0;
     flush(tb, 64 * HD);
     const int32_t* cn = M.cells + c * NN;
+    // the cell's nodal displacements once (not per point): F_q = I + (sum_b u_b dphi_b(q)^T) Ji
+    double ue[NN][GD];
+#pragma unroll
+    for (int b = 0; b < NN; ++b) {
+      const int64_t n = cn[b];
+#pragma unroll
+      for (int i = 0; i < GD; ++i) ue[b][i] = F.u[n * GD + i];
+    }
     for (int q = 0; q < NQ; ++q) {
+      double Gr[GD][GD];
+#pragma unroll
+      for (int i = 0; i < GD; ++i)
+#pragma unroll
+        for (int k = 0; k < GD; ++k) Gr[i][k] = 0.0;
+      const double* dq = tab + NQ + q * NN * GD;
+#pragma unroll
+      for (int b = 0; b < NN; ++b)
+#pragma unroll
+        for (int i = 0; i < GD; ++i)
+#pragma unroll
+          for (int k = 0; k < GD; ++k) Gr[i][k] = fma(ue[b][i], dq[b * GD + k], Gr[i][k]);
       double Fq[N];
-      deformation_gradient<GD>(F.u, cn, NN, tab + NQ + q * NN * GD, Ji, Fq);
+#pragma unroll
+      for (int i = 0; i < GD; ++i)
+#pragma unroll
+        for (int d = 0; d < GD; ++d) {
+          double f = i == d ? 1.0 : 0.0;
+#pragma unroll
+          for (int k = 0; k < GD; ++k) f = fma(Gr[i][k], Ji[k][d], f);
+          Fq[i * GD + d] = f;
+        }
       double I1 = GD == 2 ? 1.0 : 0.0, J;
 #pragma unroll
       for (int m = 0; m < N; ++m) I1 = fma(Fq[m], Fq[m], I1);
@@ -3285,6 +3366,17 @@ __global__ __launch_bounds__(256) void k_neo_records_m(MeshView M, FormView F, c
 // timing-only ablations of k_gather_neo (wrong results): 2 no accumulator adds, 4 no chunk stores
 #ifndef FA_NEOM_ABL
 #define FA_NEOM_ABL 0
+#endif
+#ifndef FA_NEOM_UONLY
+#define FA_NEOM_UONLY 0
+#endif
+#ifndef FA_NEOM_ROLL
+#define FA_NEOM_ROLL 0
+#endif
+#if FA_NEOM_ROLL
+#define FA_NEOM_ROLL_UNROLL 1
+#else
+#define FA_NEOM_ROLL_UNROLL 16
 #endif
 template <int GD, int NN, int NQ, int NSPLIT>
 __global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P, const uint32_t* __restrict__ zero32,
@@ -3397,7 +3489,8 @@ __global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
       const int aloc = pf0 % NN;
       const uint32_t rowm = (cur.mask >> (aloc * GD)) & ((1u << GD) - 1);
       const double sc = cur.hd[NT];
-      // per point: U = M_q dphi_a, W = s_c U, Z = rho_q U
+      // per point: U = M_q dphi_a, W = s_c U, Z = rho_q U (FA_NEOM_UONLY: U only, s_c V and rho_q V
+      // formed per block: 6 more multiplies per point and block, 12 fewer live doubles)
       double W[NQ][GD], Z[NQ][GD];
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
@@ -3409,15 +3502,25 @@ __global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
           double u = cur.pt[q][i * GD] * pa[0];
 #pragma unroll
           for (int kk = 1; kk < GD; ++kk) u = fma(cur.pt[q][i * GD + kk], pa[kk], u);
-          W[q][i] = sc * u;
-          Z[q][i] = cur.pt[q][BS2] * u;
+          W[q][i] = FA_NEOM_UONLY ? u : sc * u;
+          Z[q][i] = FA_NEOM_UONLY ? 0.0 : cur.pt[q][BS2] * u;
         }
       }
       lds_vdouble* Ta = (lds_vdouble*)(s_T + aloc * NN * NT);
+      // FA_NEOM_ROLL: the column loop rolled (the item's slots rotate through sl[0]): one block's
+      // values live at a time instead of the compiler's cross-block schedule
+      uint32_t slr[NBG];
 #pragma unroll
+      for (int bb = 0; bb < NBG; ++bb) slr[bb] = cur.sl[bb];
+#pragma unroll FA_NEOM_ROLL_UNROLL
       for (int bb = 0; bb < NBG; ++bb) {
-        const int s = (int)(cur.sl[bb] & 1023u);
-        const int b = (int)(cur.sl[bb] >> 10);
+        const uint32_t slv = FA_NEOM_ROLL ? slr[0] : cur.sl[bb < NBG ? bb : 0];
+        if constexpr (FA_NEOM_ROLL) {
+#pragma unroll
+          for (int t = 0; t + 1 < NBG; ++t) slr[t] = slr[t + 1];
+        }
+        const int s = (int)(slv & 1023u);
+        const int b = (int)(slv >> 10);
         lds_vdouble* pb = (lds_vdouble*)(s_phi + b * NQ * GD);
         double K[GD][GD];
 #pragma unroll
@@ -3436,10 +3539,23 @@ __global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
             for (int kk = 1; kk < GD; ++kk) v = fma(cur.pt[q][i * GD + kk], pbq[kk], v);
             V[i] = v;
           }
+          if constexpr (FA_NEOM_UONLY) {
+            double sV[GD], rV[GD];
 #pragma unroll
-          for (int i = 0; i < GD; ++i)
+            for (int i = 0; i < GD; ++i) {
+              sV[i] = sc * V[i];
+              rV[i] = cur.pt[q][BS2] * V[i];
+            }
 #pragma unroll
-            for (int kk = 0; kk < GD; ++kk) K[i][kk] = fma(W[q][i], V[kk], fma(-V[i], Z[q][kk], K[i][kk]));
+            for (int i = 0; i < GD; ++i)
+#pragma unroll
+              for (int kk = 0; kk < GD; ++kk) K[i][kk] = fma(W[q][i], sV[kk], fma(-rV[i], W[q][kk], K[i][kk]));
+          } else {
+#pragma unroll
+            for (int i = 0; i < GD; ++i)
+#pragma unroll
+              for (int kk = 0; kk < GD; ++kk) K[i][kk] = fma(W[q][i], V[kk], fma(-V[i], Z[q][kk], K[i][kk]));
+          }
         }
         double dot = 0.0;
 #pragma unroll
@@ -3472,6 +3588,9 @@ __global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
     // issued before chunk k's stores (their wait at chunk k+1 does not include the stores)
     load_item(d1, pf1, cur);
     __syncthreads();  // B1: the chunk is accumulated
+    if constexpr (FA_DRAIN_NEO && FA_NEOM_ABL != 4) {
+      chunk_drain<SW>(acc, h, nb * BS2, P.A.data + off, dump, tid);
+    } else {
     const int nv = nb * BS2;
     const int np = (nv - h) >> 1;
     dv2 v[SW];
@@ -3495,6 +3614,7 @@ __global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
     lin_store(hv, out);
     lin_store(tv, out + max(nv - 1, 0));
 #endif
+    }
     __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics
     d0 = d1;
     d1 = d2;
@@ -4404,6 +4524,12 @@ __global__ void k_plan_colors_stats(const int64_t* __restrict__ row_start, const
 #ifndef FA_P1TET_NSPLIT
 #define FA_P1TET_NSPLIT 1  // P1 tetrahedra: whole entries (4 blocks per item); config C 1.86 vs 1.97 ms (2), 2.25 (4)
 #endif
+// k_gather_lin's workgroup size (one item per thread, chunks of up to NT / NSPLIT entries): P1
+// tetrahedra have 4-block items, so their chunks are short on work per barrier at 256 items
+#ifndef FA_P1TET_NT
+#define FA_P1TET_NT 256  // 512 measured 1.72 vs 1.68 ms on config C
+#endif
+__host__ __device__ constexpr int lin_threads(int gd, int nn) { return gd == 3 && nn == 4 ? FA_P1TET_NT : 256; }
 static int lin_simplex_nsplit(int ct, int p, int nq, bool affine = false) {
   // affine hexahedra (MAT_AFFT): Q1 / Q2 / Q3 with their default rules
   if (affine && ct == FA_HEXAHEDRON && p == 1 && nq == 8) return 2;
@@ -4433,7 +4559,7 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   if (ns == 0 || plan->nchunks <= 0) return FA_OK;  // no kernel reads an ordered map: keep plain slots
   // ordered entries pack (b << 10) | chunk-relative position (k_order_slots): keep the plain map
   // for a plan whose chunks could hold 1024 blocks or more
-  if (plan->max_blocks >= 1024 || kGatherLdsValues / (8 * mesh->gdim * mesh->gdim) >= 1024) return FA_OK;
+  if (plan->max_blocks >= 1024 || gather_maxb(false, mesh->gdim * mesh->gdim) >= 1024) return FA_OK;
   const int groups = (kGatherMaxAdj * ns + 15) / 16;
   hipStream_t s = (hipStream_t)stream;
   const int64_t total = plan->nchunks * groups;
@@ -4629,7 +4755,7 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
     int rc = get_tables(mesh->cell_type, mesh->degree, -1, &T);
     if (rc) return rc;
     const int ns = lin_simplex_nsplit(mesh->cell_type, mesh->degree, T.nq);
-    if (ns > 0 && lin_gather_enabled()) maxadj = std::min(maxadj, 256 / ns);
+    if (ns > 0 && lin_gather_enabled()) maxadj = std::min(maxadj, lin_threads(mesh->gdim, mesh->nn) / ns);
   }
   return plan_gather(mesh, adj, A, row_start, plan, stream, gather_maxb(false, mesh->gdim * mesh->gdim), maxadj);
 }
@@ -5068,7 +5194,7 @@ static int chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
 // chunk (capped below the 2^32 work-item limit; larger plans loop). FEMASM_GATHER_GRID_MULT=m
 // scales the persistent grid (measurement knob).
 template <typename K>
-static int64_t gather_grid(K kernel, int64_t nchunks) {
+static int64_t gather_grid(K kernel, int64_t nchunks, int block = 256) {
   const int64_t per = (nchunks + 7) / 8;
   const char* env = getenv("FEMASM_GATHER_GRID_MULT");
   if (!gather_dynamic()) return std::min<int64_t>(8 * per, kMaxBlocks);  // kMaxBlocks % 8 == 0
@@ -5076,7 +5202,7 @@ static int64_t gather_grid(K kernel, int64_t nchunks) {
   if (hipGetDevice(&dev) == hipSuccess) {
     int v = 0;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kernel, 256, 0) == hipSuccess && v > 0) occ = v;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kernel, block, 0) == hipSuccess && v > 0) occ = v;
   }
   const double mult = (env && atof(env) > 0) ? atof(env) : 1.0;
   int64_t g = (int64_t)(cus * occ * mult);
@@ -5135,6 +5261,10 @@ static bool neo_m_enabled() {
   return !(e && e[0] == '0');
 }
 
+static bool neo_m_plan_ok(const GatherArgs& P, int nsplit) {
+  return P.eadj && P.slots && P.slot_order == nsplit && !P.cw && P.plan_maxadj >= 0 && P.plan_maxadj * nsplit <= 256;
+}
+
 template <int GD, int NN, int NQ, int NSPLIT>
 static int launch_gather_neo(GatherArgs P, const int8_t* bc, hipStream_t s, const GatherStage& W) {
   using R = NeoM<GD, NQ>;
@@ -5146,7 +5276,7 @@ static int launch_gather_neo(GatherArgs P, const int8_t* bc, hipStream_t s, cons
   }
   const bool rows = P.nchunks > 0 && W.mode != GatherStage::PREP;
   if (rows) {  // the kernel's plan: positional, ordered for NSPLIT, <= 256 items per chunk
-    if (!(P.eadj && P.slots && P.slot_order == NSPLIT && !P.cw && P.plan_maxadj >= 0 && P.plan_maxadj * NSPLIT <= 256))
+    if (!neo_m_plan_ok(P, NSPLIT))
       return fail(FA_E_ARG, "the neo-Hookean gather needs a positional plan ordered for %d column parts with <= %d "
                   "entries per chunk (fa_plan_gather_form + fa_plan_slots + fa_plan_order), or FEMASM_NEO_M=0",
                   NSPLIT, 256 / NSPLIT);
@@ -5224,7 +5354,9 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   if constexpr (MAT == FA_NEO_HOOKEAN && R::SIMP && NN % NSPLIT == 0 && NN * GD <= 32 && NN < 64) {
     // the neo-Hookean M gather (k_gather_neo) and its records: chosen per process (FEMASM_NEO_M=0
     // keeps k_gather's neo items), since the prepare stage of the split ABI has no plan
-    if (neo_m_enabled()) return launch_gather_neo<GD, NN, NQ, NSPLIT>(P, bc, s, W);
+    // fa_assemble_matrix (both stages here) with a plan the M gather cannot run keeps k_gather's items
+    if (neo_m_enabled() && (W.mode != GatherStage::FULL || neo_m_plan_ok(P, NSPLIT)))
+      return launch_gather_neo<GD, NN, NQ, NSPLIT>(P, bc, s, W);
   }
   const int64_t nc = P.M.ncells;
   const int64_t rec_bytes = align256((int64_t)sizeof(double) * R::count(nc));
@@ -5253,8 +5385,9 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   P.bcmask = mask;
   if constexpr (MAT == MAT_LINU && R::SIMP && NN % NSPLIT == 0 && NN * GD <= 32 && NN < 64) {
     // the store-decoupled gather (k_gather_lin): positional plans of <= 256 items per chunk
+    constexpr int LNT = lin_threads(GD, NN);
     if (P.nchunks > 0 && W.mode != GatherStage::PREP && !P.cw && lin_gather_enabled() && P.eadj && P.slots &&
-        P.slot_order == NSPLIT && !P.corder && P.plan_maxadj * NSPLIT <= 256 && P.plan_maxadj >= 0) {
+        P.slot_order == NSPLIT && !P.corder && P.plan_maxadj * NSPLIT <= LNT && P.plan_maxadj >= 0) {
       if (P.plan_maxb > gather_maxb(false, GD * GD))
         return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, the kernel %d", P.plan_maxb,
                     gather_maxb(false, GD * GD));
@@ -5270,9 +5403,9 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       uint32_t* zero32 = nullptr;
       double* dump = nullptr;
       if ((rc = lin_scratch(&zero32, &dump))) return rc;
-      const int64_t grid = gather_grid(k_gather_lin<GD, NN, NSPLIT>, P.nchunks);
+      const int64_t grid = gather_grid(k_gather_lin<GD, NN, NSPLIT, LNT>, P.nchunks, LNT);
       const int64_t per = (P.nchunks + grid - 1) / grid;
-      k_gather_lin<GD, NN, NSPLIT><<<(unsigned)grid, 256, 0, s>>>(P, zero32, dump, per);
+      k_gather_lin<GD, NN, NSPLIT, LNT><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, per);
       LAUNCH_CHECK();
       if (bc) {  // Dirichlet diagonals (dolfinx set_diagonal) of the plan's rows
         k_bc_diag<GD><<<grid_for((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
