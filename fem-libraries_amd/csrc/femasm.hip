@@ -833,20 +833,48 @@ typedef double fa_d4 __attribute__((ext_vector_type(4)));
 // the 256 VGPRs of 2 waves / SIMD (16 waves of one tile were capped at 128 VGPRs and spilled 35)
 __host__ __device__ constexpr int hex_tpw(int nn) { return ((nn + 15) / 16) * ((nn + 15) / 16) >= 16 ? 2 : 1; }
 __host__ __device__ constexpr int hex_threads(int nn) { return 64 * ((nn + 15) / 16) * ((nn + 15) / 16) / hex_tpw(nn); }
+// MODE 2 (block store for the row gather) computes the upper-triangle tiles only (ta <= tb: 10 of 16
+// for Q3) and stores each off-diagonal tile twice, as itself and transposed (K_ba = K_ab^T: M_ik[a][b]
+// = Phi_i[a] . Phi_k[b] = M_ki[b][a]); FA_HEX_UPPER=0 computes every tile
+#ifndef FA_HEX_UPPER
+#define FA_HEX_UPPER 0  // 1 measured slower on config Dmfma: k_hex_mfma 27.5 -> 38.5 ms (5-wave workgroups at
+                        // 2 waves / SIMD leave 3 of a CU's 8 wave slots idle; transposed stores of 288-B runs)
+#endif
+__host__ __device__ constexpr int hex_ntiles(int nn, int mode) {
+  return (mode == 2 && FA_HEX_UPPER) ? ((nn + 15) / 16) * ((nn + 15) / 16 + 1) / 2 : ((nn + 15) / 16) * ((nn + 15) / 16);
+}
+__host__ __device__ constexpr int hex_threads_m(int nn, int mode) {
+  return 64 * ((hex_ntiles(nn, mode) + hex_tpw(nn) - 1) / hex_tpw(nn));
+}
 
 template <int NN, int NQ, int MODE>
-__global__ __launch_bounds__(hex_threads(NN)) void k_hex_mfma(
+__global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
     MeshView M, FormView F, DevTables T, int64_t c0, int64_t ncells, double* __restrict__ Ae, BsrView A,
     const int8_t* __restrict__ bc, int* __restrict__ err) {
   constexpr int NT = (NN + 15) / 16;  // 16-row tiles per side; TPW (a, b) tiles per wave
-  constexpr int TPW = hex_tpw(NN), NWAVE = NT * NT / TPW;
-  constexpr int NTHR = hex_threads(NN);
+  constexpr bool UPPER = MODE == 2 && FA_HEX_UPPER;
+  constexpr int NTL = hex_ntiles(NN, MODE);  // tiles computed
+  constexpr int TPW = hex_tpw(NN), NWAVE = (NTL + TPW - 1) / TPW;
+  constexpr int NTHR = hex_threads_m(NN, MODE);
+  // tile t -> (ta, tb): row-major over the full grid, or over the upper triangle (UPPER)
+  auto tile_of = [](int t, int& ta, int& tb) {
+    if constexpr (UPPER) {
+      int r = 0, rem = t < NTL ? t : NTL - 1;
+      while (rem >= NT - r) { rem -= NT - r; ++r; }
+      ta = r;
+      tb = r + rem;
+    } else {
+      ta = t / NT;
+      tb = t % NT;
+    }
+  };
   constexpr int NNP = NT * 16 + 16;   // row stride: +16 doubles puts q and q+1 on opposite bank halves
   constexpr int QMAX = (NQ + 3) & ~3;
   __shared__ double phi[3][QMAX][NNP];
   __shared__ double sJ[QMAX][10];  // Ji (9) + sqrt(w |J|)
   __shared__ uint8_t s_bcn[NN];    // MODE 2: constrained-dof bits of the cell's nodes
   static_assert(MODE != 2 || 3 * QMAX * NNP >= NWAVE * 64 * 9, "block staging fits the phi image");
+  static_assert(NTL % TPW == 0, "whole waves of tiles");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nq = NQ, nqp = QMAX;
   for (int64_t ci = blockIdx.x; ci < ncells; ci += gridDim.x) {
@@ -903,7 +931,8 @@ __global__ __launch_bounds__(hex_threads(NN)) void k_hex_mfma(
       for (int q0 = 0; q0 < nqp; q0 += 4) {
 #pragma unroll
         for (int j = 0; j < TPW; ++j) {
-          const int t = wave + j * NWAVE, ta = t / NT, tb = t % NT;
+          int ta, tb;
+          tile_of(wave + j * NWAVE, ta, tb);
           const int ra = ta * 16 + (lane & 15), rb = tb * 16 + (lane & 15);
           double av[3], bv[3];
 #pragma unroll
@@ -922,8 +951,8 @@ __global__ __launch_bounds__(hex_threads(NN)) void k_hex_mfma(
     if constexpr (MODE == 2) __syncthreads();  // every wave is past its MFMA loop: phi is free
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
-      const int t = wave + j * NWAVE;
-      const int ta = t / NT, tb = t % NT;
+      int ta, tb;
+      tile_of(wave + j * NWAVE, ta, tb);
       const fa_d4 (&acc)[9] = accs[j];
       // D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * r
       if constexpr (MODE == 2) {
@@ -960,6 +989,32 @@ __global__ __launch_bounds__(hex_threads(NN)) void k_hex_mfma(
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          if (UPPER && ta != tb) {
+            // the transposed tile: block (b, a) = K_ab^T; row b holds the 4 blocks a = ta*16 + 4r + {0..3}
+            if (a < NN && b < NN) {
+              const double tr = acc[0][r] + acc[4][r] + acc[8][r];
+              const uint32_t rm = s_bcn[a], cm = s_bcn[b];
+#pragma unroll
+              for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                  const double v = lam * acc[i * 3 + k][r] + mu * acc[k * 3 + i][r] + (i == k ? mu * tr : 0.0);
+                  st[(lane & 15) * 36 + (lane >> 4) * 9 + k * 3 + i] = (((rm >> i) | (cm >> k)) & 1u) ? 0.0 : v;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int nav = min(4, NN - (ta * 16 + 4 * r)) * 9;  // valid values of a row run
+            for (int t = lane; t < 16 * 36; t += 64) {
+              const int j = t / 36, off = t - j * 36;
+              const int bj = tb * 16 + j;
+              if (bj < NN && off < nav) Ae[((ci * NN + bj) * NN + ta * 16 + 4 * r) * 9 + off] = st[t];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          }
         }
         continue;
       }
@@ -1023,7 +1078,7 @@ static int launch_hex_mfma(int mode, const fa_mesh* mesh, const MeshView& M, con
   do {                                                                                                        \
     constexpr int thr = hex_threads(NN);                                                                      \
     if (mode == 0) k_hex_mfma<NN, NQ, 0><<<grid, thr, 0, s>>>(M, F, T, c0, nc, Ae, A, bc, derr);               \
-    else if (mode == 2) k_hex_mfma<NN, NQ, 2><<<grid, thr, 0, s>>>(M, F, T, c0, nc, Ae, A, bc, derr);          \
+    else if (mode == 2) k_hex_mfma<NN, NQ, 2><<<grid, hex_threads_m(NN, 2), 0, s>>>(M, F, T, c0, nc, Ae, A, bc, derr); \
     else k_hex_mfma<NN, NQ, 1><<<grid, thr, 0, s>>>(M, F, T, c0, nc, Ae, A, bc, derr);                        \
   } while (0)
   // the default (UFL-estimated) rules: Q1 2^3, Q2 3^3, Q3 4^3 points
@@ -1095,6 +1150,12 @@ static constexpr int kGatherMaxRows = 128;      // rows per chunk
 // gather variant whose blocks come from a per-cell block store [cell][a][b][GD][GD] (hexahedra:
 // written by the MFMA kernel) instead of being computed from a record
 constexpr int MAT_BLOCKS = 9;
+#ifndef FA_EB_WAVE
+#define FA_EB_WAVE 1  // MAT_BLOCKS: one wave per adjacency entry (coalesced block-store reads), 0: lane items
+#endif
+#ifndef FA_EB_UNROLL
+#define FA_EB_UNROLL 2
+#endif
 // linear elasticity with one Poisson ratio for all cells (E per cell): lam / mu = r is uniform, so
 // lam G + mu G^T = mu |J| Ji^T (r Ahat + Ahat^T) Ji; the record holds s Ji with s^2 = mu |J|
 // (and the sign of mu |J|), the table B_ab = r Ahat_ab + Ahat_ab^T, and
@@ -2715,7 +2776,50 @@ void k_gather(GatherArgs P) {
       it0 += 256;
     }
 #if FA_ABL != 6
-    if constexpr (BARY) {
+    if constexpr (MAT == MAT_BLOCKS && FA_EB_WAVE) {
+      if (P.slots) {
+        // element blocks: one wave per adjacency entry, its NN blocks (NN * 9 contiguous values of
+        // Eb[c][a][.]) streamed with coalesced 8-B-per-lane loads, one LDS add per value (a lane's
+        // block b = idx / 9 and entry e = idx % 9), instead of one lane reading NSPLIT whole blocks
+        const int lane = tid & 63, wv = tid >> 6;
+        constexpr int NEV = NN * BS2, NR = (NEV + 63) / 64;
+        // FA_EB_UNROLL entries per wave in flight (their loads issued together)
+        for (int j0 = wv * FA_EB_UNROLL; j0 < na; j0 += 4 * FA_EB_UNROLL) {
+          double v[FA_EB_UNROLL][NR];
+          int sl[FA_EB_UNROLL][NR], lo[FA_EB_UNROLL];
+#pragma unroll
+          for (int w = 0; w < FA_EB_UNROLL; ++w) {
+            const int j = min(j0 + w, na - 1);
+            const int32_t pflat = s_adj[j];
+            const int64_t c = pflat / NN;
+            const int aloc = pflat % NN;
+            lo[w] = rowoff[adjrow[j]];
+            const double* Eb = P.rec + ((int64_t)c * NN + aloc) * NEV;
+            const uint16_t* sr = P.slots + ((int64_t)a0 + j) * NN;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+              const int idx = min(lane + 64 * r, NEV - 1);
+              v[w][r] = __builtin_nontemporal_load(Eb + idx);
+              sl[w][r] = (int)sr[idx / BS2];
+            }
+          }
+#pragma unroll
+          for (int w = 0; w < FA_EB_UNROLL; ++w) {
+            if (j0 + w >= na) break;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+              const int idx = lane + 64 * r;
+              if (idx < NEV) {
+                const int b = idx / BS2, e = idx - b * BS2;
+                atomicAdd(&acc[(lo[w] + sl[w][r]) * BS2 + e], v[w][r]);
+              }
+            }
+          }
+        }
+      } else {
+        for (; it0 < nitems; it0 += 256) item(it0, std::false_type{});
+      }
+    } else if constexpr (BARY) {
       // part = tid / (256 / NSPLIT): whole waves per part; entry jj of the chunk on lane tid % (256 / NSPLIT)
       constexpr int LPP = 256 / NSPLIT;
       for (int jj = tid % LPP; jj < na; jj += LPP) item(jj * NSPLIT + tid / LPP, std::false_type{});
@@ -3371,24 +3475,44 @@ __global__ __launch_bounds__(256) void k_neo_records_m(MeshView M, FormView F, c
 #define FA_NEOM_UONLY 0
 #endif
 #ifndef FA_NEOM_ROLL
-#define FA_NEOM_ROLL 0
+#define FA_NEOM_ROLL 0  // with FA_NEOM_QS=2 (and FA_NEOM_UONLY=1): the spill-free q-split build
 #endif
 #if FA_NEOM_ROLL
 #define FA_NEOM_ROLL_UNROLL 1
 #else
 #define FA_NEOM_ROLL_UNROLL 16
 #endif
-template <int GD, int NN, int NQ, int NSPLIT>
-__global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P, const uint32_t* __restrict__ zero32,
-                                                                  double* __restrict__ dump) {
+// Q-split items (QS = 2, P2 tetrahedra): each (entry, column part) item runs on a lane pair, one
+// lane per half of the quadrature points (half the record and the per-point W, Z in registers:
+// 4 instead of 2 waves / SIMD); the pair sums its partial blocks by DPP and each lane adds half of
+// the 9 entries into LDS. 512-thread workgroups keep 256 items (the neo plan's 128 entries) per chunk.
+#ifndef FA_NEOM_QS
+#define FA_NEOM_QS 1  // 2: q-split lane pairs, measured slower (E-neo 94 vs 77 ms: DPP sums and a rolled column loop, VALU +84 %)
+#endif
+template <int NQ>
+__host__ __device__ constexpr int neo_qsplit() { return NQ % FA_NEOM_QS == 0 ? FA_NEOM_QS : 1; }
+// the lane pair's sum of a double (quad_perm [1, 0, 3, 2]: swap with the neighbouring lane)
+__device__ __forceinline__ double pair_sum(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int plo = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false);
+  const int phi = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false);
+  return v + __hiloint2double(phi, plo);
+}
+template <int GD, int NN, int NQ, int NSPLIT, int QS = 1>
+__global__ __launch_bounds__(256 * QS, QS == 2 ? 4 : FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
+                                                                                  const uint32_t* __restrict__ zero32,
+                                                                                  double* __restrict__ dump) {
   using R = NeoM<GD, NQ>;
-  constexpr int BS2 = GD * GD, NT = R::NT;
+  constexpr int NTH = 256 * QS;  // threads: 256 items
+  constexpr int BS2 = GD * GD, NT = R::NT, NQL = NQ / QS;
   constexpr int NBG = NN / NSPLIT;
   constexpr int MAXB = gather_maxb(true, BS2);
   constexpr int NACC = MAXB * BS2 + 2;
   constexpr int NP2 = (NACC + 1) / 2;
-  constexpr int SW = (MAXB * BS2 / 2 + 255) / 256;
-  static_assert(NN % NSPLIT == 0 && NN * GD <= 32 && NN <= 63 && MAXB < 1024, "k_gather_neo: affine simplices");
+  constexpr int SW = (MAXB * BS2 / 2 + NTH - 1) / NTH;
+  constexpr int NE = (BS2 + QS - 1) / QS;  // block entries each lane of an item adds
+  static_assert(NN % NSPLIT == 0 && NN * GD <= 32 && NN <= 63 && MAXB < 1024 && NQ % QS == 0 && QS <= 2,
+                "k_gather_neo: affine simplices");
   typedef double dv2 __attribute__((ext_vector_type(2)));
   __shared__ __attribute__((aligned(16))) double acc[2 * NP2];
   __shared__ double s_phi[NN * NQ * GD];  // [b][q][k]: a column's gradients at every point, contiguous
@@ -3402,11 +3526,11 @@ __global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
   if (cnt == 0) return;
   const double* wq = P.tab;
   const double* dphi = P.tab + NQ;  // [q][b][k]
-  for (int t = tid; t < NN * NQ * GD; t += 256) {
+  for (int t = tid; t < NN * NQ * GD; t += NTH) {
     const int b = t / (NQ * GD), q = (t / GD) % NQ, k = t % GD;
     s_phi[t] = dphi[(q * NN + b) * GD + k];
   }
-  for (int t = tid; t < NN * NN; t += 256) {
+  for (int t = tid; t < NN * NN; t += NTH) {
     const int a = t / NN, b = t % NN;
     double Ah[GD][GD];
 #pragma unroll
@@ -3423,7 +3547,7 @@ __global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
 #pragma unroll
       for (int l = j; l < GD; ++l) s_T[t * NT + sym_pair<GD>(j, l)] = j == l ? Ah[j][j] : Ah[j][l] + Ah[l][j];
   }
-  for (int t = tid; t < NP2; t += 256) acc2[t] = dv2{0.0, 0.0};
+  for (int t = tid; t < NP2; t += NTH) acc2[t] = dv2{0.0, 0.0};
 
   const int64_t abase = sload(P.A.indptr, P.A.row_begin);
   const int64_t nent = P.M.ncells * NN;
@@ -3437,36 +3561,41 @@ __global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
     const int64_t r0 = sload(P.row_start, c), r1 = sload(P.row_start, c + 1);
     return Desc{sload(P.A.indptr, r0), sload(P.A.indptr, r1), sload(P.adj_ptr, r0), sload(P.adj_ptr, r1)};
   };
-  const int jit = tid / NSPLIT, part = tid % NSPLIT;
+  const int item = tid / QS, qh = tid % QS;  // qh: this lane's half of the points
+  const int jit = item / NSPLIT, part = item % NSPLIT;
   auto entry_of = [&](const Desc& d) -> int64_t {
     const int na = (int)(d.a1 - d.a0);
     int64_t e = d.a0 + min(jit, max(na - 1, 0));
     return min(max(e, (int64_t)0), nent - 1);
   };
   auto load_entry = [&](const Desc& d) -> int32_t { return eadj[entry_of(d)]; };
-  struct Item { double hd[R::HEAD]; double pt[NQ][R::PT]; uint32_t sl[NBG]; uint32_t mask; };
+  // the head's S and s_c (NT + 1 values; its padding is not loaded); slots two per register
+  constexpr int HL = NT + 1, NSL = (NBG + 1) / 2;
+  struct Item { double hd[HL]; double pt[NQL][R::PT]; uint32_t sl[NSL]; uint32_t mask; };
   auto load_item = [&](const Desc& d, int32_t pflat, Item& it) {
     const int64_t c = pflat / NN;
-    const dv2* hp = reinterpret_cast<const dv2*>(P.rec + R::head(c));
+    const double* hq = P.rec + R::head(c);
+    const dv2* hp = reinterpret_cast<const dv2*>(hq);
 #pragma unroll
-    for (int k = 0; k < R::HEAD / 2; ++k) {
+    for (int k = 0; k < HL / 2; ++k) {
       const dv2 v = hp[k];
       it.hd[2 * k] = v.x;
       it.hd[2 * k + 1] = v.y;
     }
+    if constexpr (HL % 2) it.hd[HL - 1] = hq[HL - 1];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const dv2* pp = reinterpret_cast<const dv2*>(P.rec + R::point(c, q));
+    for (int ql = 0; ql < NQL; ++ql) {
+      const dv2* pp = reinterpret_cast<const dv2*>(P.rec + R::point(c, qh * NQL + ql));
 #pragma unroll
       for (int k = 0; k < R::PT / 2; ++k) {
         const dv2 v = pp[k];
-        it.pt[q][2 * k] = v.x;
-        it.pt[q][2 * k + 1] = v.y;
+        it.pt[ql][2 * k] = v.x;
+        it.pt[ql][2 * k + 1] = v.y;
       }
     }
     const uint16_t* sp = P.slots + entry_of(d) * NN + part * NBG;
 #pragma unroll
-    for (int bb = 0; bb < NBG; ++bb) it.sl[bb] = sp[bb];
+    for (int t = 0; t < NSL; ++t) it.sl[t] = (uint32_t)sp[2 * t] | (2 * t + 1 < NBG ? (uint32_t)sp[2 * t + 1 < NBG ? 2 * t + 1 : 0] << 16 : 0u);
     it.mask = mk[c * mkmul] * mkmul;
   };
 
@@ -3491,52 +3620,64 @@ __global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
       const double sc = cur.hd[NT];
       // per point: U = M_q dphi_a, W = s_c U, Z = rho_q U (FA_NEOM_UONLY: U only, s_c V and rho_q V
       // formed per block: 6 more multiplies per point and block, 12 fewer live doubles)
-      double W[NQ][GD], Z[NQ][GD];
+      double W[NQL][GD], Z[NQL][GD];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
+      for (int ql = 0; ql < NQL; ++ql) {
+        const int q = qh * NQL + ql;
         double pa[GD];
 #pragma unroll
         for (int kk = 0; kk < GD; ++kk) pa[kk] = s_phi[(aloc * NQ + q) * GD + kk];
 #pragma unroll
         for (int i = 0; i < GD; ++i) {
-          double u = cur.pt[q][i * GD] * pa[0];
+          double u = cur.pt[ql][i * GD] * pa[0];
 #pragma unroll
-          for (int kk = 1; kk < GD; ++kk) u = fma(cur.pt[q][i * GD + kk], pa[kk], u);
-          W[q][i] = FA_NEOM_UONLY ? u : sc * u;
-          Z[q][i] = FA_NEOM_UONLY ? 0.0 : cur.pt[q][BS2] * u;
+          for (int kk = 1; kk < GD; ++kk) u = fma(cur.pt[ql][i * GD + kk], pa[kk], u);
+          W[ql][i] = FA_NEOM_UONLY ? u : sc * u;
+          Z[ql][i] = FA_NEOM_UONLY ? 0.0 : cur.pt[ql][BS2] * u;
         }
       }
       lds_vdouble* Ta = (lds_vdouble*)(s_T + aloc * NN * NT);
-      // FA_NEOM_ROLL: the column loop rolled (the item's slots rotate through sl[0]): one block's
-      // values live at a time instead of the compiler's cross-block schedule
-      uint32_t slr[NBG];
+      const double dsel = qh == 0 ? 1.0 : 0.0;  // the mu term once per item
+      // rolled loop: the mu-term dots of the item's columns up front (S dies here), rotated per block
+      double dt[NBG];
+      if constexpr (FA_NEOM_ROLL) {
 #pragma unroll
-      for (int bb = 0; bb < NBG; ++bb) slr[bb] = cur.sl[bb];
+        for (int bb = 0; bb < NBG; ++bb) {
+          const int b = (int)((cur.sl[bb / 2] >> (16 * (bb % 2) + 10)) & 63u);
+          double dd = 0.0;
+#pragma unroll
+          for (int t = 0; t < NT; ++t) dd = fma(cur.hd[t], Ta[b * NT + t], dd);
+          dt[bb] = dsel * dd;
+        }
+      }
+      // QS = 2: the column loop rolled (FA_NEOM_ROLL): one block's values live at a time
 #pragma unroll FA_NEOM_ROLL_UNROLL
       for (int bb = 0; bb < NBG; ++bb) {
-        const uint32_t slv = FA_NEOM_ROLL ? slr[0] : cur.sl[bb < NBG ? bb : 0];
+        uint32_t slv;
         if constexpr (FA_NEOM_ROLL) {
-#pragma unroll
-          for (int t = 0; t + 1 < NBG; ++t) slr[t] = slr[t + 1];
+          const uint64_t w01 = (uint64_t)cur.sl[0] | ((uint64_t)cur.sl[NSL > 1 ? 1 : 0] << 32);
+          slv = bb < 4 ? (uint32_t)(w01 >> (16 * bb)) & 0xFFFFu : (cur.sl[NSL - 1] >> 16 * (bb & 1)) & 0xFFFFu;
+        } else {
+          slv = (cur.sl[bb / 2] >> (16 * (bb % 2))) & 0xFFFFu;
         }
         const int s = (int)(slv & 1023u);
         const int b = (int)(slv >> 10);
-        lds_vdouble* pb = (lds_vdouble*)(s_phi + b * NQ * GD);
+        lds_vdouble* pb = (lds_vdouble*)(s_phi + (b * NQ + qh * NQL) * GD);
         double K[GD][GD];
 #pragma unroll
         for (int i = 0; i < GD; ++i)
 #pragma unroll
           for (int kk = 0; kk < GD; ++kk) K[i][kk] = 0.0;
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
+        for (int ql = 0; ql < NQL; ++ql) {
           double pbq[GD], V[GD];
 #pragma unroll
-          for (int kk = 0; kk < GD; ++kk) pbq[kk] = pb[q * GD + kk];
+          for (int kk = 0; kk < GD; ++kk) pbq[kk] = pb[ql * GD + kk];
 #pragma unroll
           for (int i = 0; i < GD; ++i) {
-            double v = cur.pt[q][i * GD] * pbq[0];
+            double v = cur.pt[ql][i * GD] * pbq[0];
 #pragma unroll
-            for (int kk = 1; kk < GD; ++kk) v = fma(cur.pt[q][i * GD + kk], pbq[kk], v);
+            for (int kk = 1; kk < GD; ++kk) v = fma(cur.pt[ql][i * GD + kk], pbq[kk], v);
             V[i] = v;
           }
           if constexpr (FA_NEOM_UONLY) {
@@ -3544,24 +3685,37 @@ __global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
 #pragma unroll
             for (int i = 0; i < GD; ++i) {
               sV[i] = sc * V[i];
-              rV[i] = cur.pt[q][BS2] * V[i];
+              rV[i] = cur.pt[ql][BS2] * V[i];
             }
 #pragma unroll
             for (int i = 0; i < GD; ++i)
 #pragma unroll
-              for (int kk = 0; kk < GD; ++kk) K[i][kk] = fma(W[q][i], sV[kk], fma(-rV[i], W[q][kk], K[i][kk]));
+              for (int kk = 0; kk < GD; ++kk) K[i][kk] = fma(W[ql][i], sV[kk], fma(-rV[i], W[ql][kk], K[i][kk]));
           } else {
 #pragma unroll
             for (int i = 0; i < GD; ++i)
 #pragma unroll
-              for (int kk = 0; kk < GD; ++kk) K[i][kk] = fma(W[q][i], V[kk], fma(-V[i], Z[q][kk], K[i][kk]));
+              for (int kk = 0; kk < GD; ++kk) K[i][kk] = fma(W[ql][i], V[kk], fma(-V[i], Z[ql][kk], K[i][kk]));
           }
         }
-        double dot = 0.0;
+        if constexpr (FA_NEOM_ROLL) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) dot = fma(cur.hd[t], Ta[b * NT + t], dot);
+          for (int i = 0; i < GD; ++i) K[i][i] += dt[0];
 #pragma unroll
-        for (int i = 0; i < GD; ++i) K[i][i] += dot;
+          for (int t = 0; t + 1 < NBG; ++t) dt[t] = dt[t + 1];
+        } else {
+          double dot = 0.0;
+#pragma unroll
+          for (int t = 0; t < NT; ++t) dot = fma(cur.hd[t], Ta[b * NT + t], dot);
+#pragma unroll
+          for (int i = 0; i < GD; ++i) K[i][i] = fma(dsel, dot, K[i][i]);
+        }
+        if constexpr (QS == 2) {
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int kk = 0; kk < GD; ++kk) K[i][kk] = pair_sum(K[i][kk]);
+        }
         const uint32_t colm = (cur.mask >> (b * GD)) & ((1u << GD) - 1);
         if (__any((rowm | colm) != 0u)) {
 #pragma unroll
@@ -3576,10 +3730,20 @@ __global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
 #if FA_NEOM_ABL == 2
           if (K[0][0] == 1.2345e-300) ap[0] = K[1][1];
 #else
+          if constexpr (QS == 1) {
 #pragma unroll
-          for (int i = 0; i < GD; ++i)
+            for (int i = 0; i < GD; ++i)
 #pragma unroll
-            for (int kk = 0; kk < GD; ++kk) atomicAdd(ap + i * GD + kk, K[i][kk]);
+              for (int kk = 0; kk < GD; ++kk) atomicAdd(ap + i * GD + kk, K[i][kk]);
+          } else {  // lane qh adds entries qh * NE .. qh * NE + NE - 1
+            const double* Kf = &K[0][0];
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+              const int e1 = NE + e;
+              const double val = qh ? (e1 < BS2 ? Kf[e1 < BS2 ? e1 : 0] : 0.0) : Kf[e];
+              if (qh == 0 || e1 < BS2) atomicAdd(ap + qh * NE + e, val);
+            }
+          }
 #endif
         }
       }
@@ -3589,18 +3753,18 @@ __global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
     load_item(d1, pf1, cur);
     __syncthreads();  // B1: the chunk is accumulated
     if constexpr (FA_DRAIN_NEO && FA_NEOM_ABL != 4) {
-      chunk_drain<SW>(acc, h, nb * BS2, P.A.data + off, dump, tid);
+      chunk_drain<SW, NTH>(acc, h, nb * BS2, P.A.data + off, dump, tid);
     } else {
     const int nv = nb * BS2;
     const int np = (nv - h) >> 1;
     dv2 v[SW];
 #pragma unroll
-    for (int u = 0; u < SW; ++u) v[u] = acc2[h + max(min(tid + 256 * u, np - 1), 0)];
+    for (int u = 0; u < SW; ++u) v[u] = acc2[h + max(min(tid + NTH * u, np - 1), 0)];
     const double hv = acc[h], tv = acc[max(nv - 1, 0) + h];
     __syncthreads();  // B2: every read is done before any zero
 #pragma unroll
     for (int u = 0; u < SW; ++u)
-      if (tid + 256 * u < np) acc2[h + tid + 256 * u] = dv2{0.0, 0.0};
+      if (tid + NTH * u < np) acc2[h + tid + NTH * u] = dv2{0.0, 0.0};
     if (tid == 0) acc2[0] = dv2{0.0, 0.0};
     if (tid == 1) acc2[(max(nv - 1, 0) + h) >> 1] = dv2{0.0, 0.0};
     const bool none = np < 1;
@@ -3610,7 +3774,7 @@ __global__ __launch_bounds__(256, FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
     if (hv == 1.2345e-300) out[0] = tv + v[0].x + v[SW - 1].y;
 #else
 #pragma unroll
-    for (int u = 0; u < SW; ++u) lin_store(v[u], out2 + max(min(tid + 256 * u, np - 1), 0));
+    for (int u = 0; u < SW; ++u) lin_store(v[u], out2 + max(min(tid + NTH * u, np - 1), 0));
     lin_store(hv, out);
     lin_store(tv, out + max(nv - 1, 0));
 #endif
@@ -5305,8 +5469,9 @@ static int launch_gather_neo(GatherArgs P, const int8_t* bc, hipStream_t s, cons
     uint32_t* zero32 = nullptr;
     double* dump = nullptr;
     if ((rc = lin_scratch(&zero32, &dump))) return rc;
-    const int64_t grid = gather_grid(k_gather_neo<GD, NN, NQ, NSPLIT>, P.nchunks);
-    k_gather_neo<GD, NN, NQ, NSPLIT><<<(unsigned)grid, 256, 0, s>>>(P, zero32, dump);
+    constexpr int QS = neo_qsplit<NQ>();
+    const int64_t grid = gather_grid(k_gather_neo<GD, NN, NQ, NSPLIT, QS>, P.nchunks, 256 * QS);
+    k_gather_neo<GD, NN, NQ, NSPLIT, QS><<<(unsigned)grid, 256 * QS, 0, s>>>(P, zero32, dump);
     LAUNCH_CHECK();
     if (bc) {  // Dirichlet diagonals (dolfinx set_diagonal) of the plan's rows
       k_bc_diag<GD><<<grid_for((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
@@ -5529,7 +5694,7 @@ static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc,
     eb = reinterpret_cast<double*>(W.work);
   }
   if (nc > 0 && W.mode != GatherStage::ROWS) {
-    constexpr int thr = hex_threads(NN);
+    constexpr int thr = hex_threads_m(NN, 2);
     const int grid = (int)std::min<int64_t>(nc, kMaxBlocks);
     BsrView none{nullptr, nullptr, nullptr, 0, 0};
     k_hex_mfma<NN, NQ, 2><<<grid, thr, 0, s>>>(P.M, P.F, T, 0, nc, eb, none, bc, P.err);
