@@ -3069,6 +3069,9 @@ __device__ __forceinline__ void chunk_drain(double* acc, int h, int nv, double* 
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rs,
                                         (tid == (jt % NT) && tail_half && !(jt == 0 && h)) ? 8 * (h + nv - 1) : OOB, 0, AUX);
 }
+#ifndef FA_LIN_P1GRAD
+#define FA_LIN_P1GRAD 1  // P1 simplices: blocks from the gradients in the record, no table (k_gather_lin)
+#endif
 #ifndef FA_LIN_ABL
 // timing-only ablations of k_gather_lin (wrong results; tools/lin_ablate.sh): 1 plain read-add-write
 // instead of LDS atomics (races), 2 no accumulator adds, 3 no table reads, 4 no chunk stores,
@@ -3087,6 +3090,7 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
   constexpr int SW = (MAXB * BS2 / 2 + NT - 1) / NT;  // pair stores per lane per chunk
   constexpr int RL = R::SIZE;
   static_assert(NN % NSPLIT == 0 && NN * GD <= 32 && RL % 2 == 0 && NN <= 63, "k_gather_lin: affine simplices");
+  constexpr bool P1G = NN == GD + 1 && FA_LIN_P1GRAD;
   typedef double dv2 __attribute__((ext_vector_type(2)));
   __shared__ __attribute__((aligned(16))) double acc[2 * NP2];
   __shared__ double tab[NN * NN * BS2];
@@ -3180,8 +3184,23 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
       lds_vdouble* Ah0 = (lds_vdouble*)(tab + aloc * NN * BS2);
       const uint32_t rowm = (cur.mask >> (aloc * GD)) & ((1u << GD) - 1);
       const bool negw = __any(cur.r[BS2] < 0.0);  // wave-uniform: a cell with mu |J| < 0
+      // P1 simplices (P1G): the scaled physical gradients are the rows of s Ji (node k >= 1) and minus
+      // their sum (node 0), so K_ab = (1/GD!) [r g_a g_b^T + g_b g_a^T + (g_a . g_b) I] without the
+      // reference-tensor table (no LDS reads; the column's gradient is selected from registers)
+      double gA[GD];
+      if constexpr (P1G) {
+#pragma unroll
+        for (int d = 0; d < GD; ++d) {
+          double g0 = 0.0;
+#pragma unroll
+          for (int kk = 0; kk < GD; ++kk) g0 -= cur.r[kk * GD + d];
+          gA[d] = g0;
+#pragma unroll
+          for (int kk = 0; kk < GD; ++kk) gA[d] = aloc == kk + 1 ? cur.r[kk * GD + d] : gA[d];
+        }
+      }
       double Bn[BS2];
-      {
+      if constexpr (!P1G) {
         const int b = (int)(cur.sl[0] >> 10);
 #pragma unroll
         for (int e = 0; e < BS2; ++e) Bn[e] = Ah0[b * BS2 + e];
@@ -3190,6 +3209,26 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
       for (int bb = 0; bb < NBG; ++bb) {
         const int s = (int)(cur.sl[bb] & 1023u);
         const int b = (int)(cur.sl[bb] >> 10);
+        double G[GD][GD];
+        if constexpr (P1G) {
+          constexpr double cv = GD == 2 ? 0.5 : 1.0 / 6.0;  // reference simplex volume
+          double gB[GD], dot = 0.0;
+#pragma unroll
+          for (int d = 0; d < GD; ++d) {
+            double g0 = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < GD; ++kk) g0 -= cur.r[kk * GD + d];
+#pragma unroll
+            for (int kk = 0; kk < GD; ++kk) g0 = b == kk + 1 ? cur.r[kk * GD + d] : g0;
+            gB[d] = g0;
+            dot = fma(gA[d], g0, dot);
+          }
+          const double ra = cv * P.rlm;
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int kk = 0; kk < GD; ++kk) G[i][kk] = fma(ra * gA[i], gB[kk], cv * gB[i] * gA[kk]) + (i == kk ? cv * dot : 0.0);
+        } else {
         double B[BS2];
 #pragma unroll
         for (int e = 0; e < BS2; ++e) B[e] = Bn[e];
@@ -3204,7 +3243,6 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
 #endif
         }
         // G = (s Ji)^T B (s Ji), column by column; K = G + tr(G) / (1 + r) I
-        double G[GD][GD];
 #pragma unroll
         for (int dd = 0; dd < GD; ++dd) {
           double T[GD];
@@ -3229,6 +3267,7 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
         tr *= P.trc;
 #pragma unroll
         for (int i = 0; i < GD; ++i) G[i][i] += tr;
+        }
         if (negw) {
           const double sg = cur.r[BS2];
 #pragma unroll
