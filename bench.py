@@ -319,23 +319,27 @@ def main():
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    # Multi-core CPU baseline workers: a fork server started before this process touches the GPU
-    # (workers must not inherit an initialised HIP runtime); used after the GPU timing.
-    cpu_pool, cpu_cores = None, 1
+    # Multi-core CPU baseline workers: the fork server starts before this process touches the GPU
+    # (workers must not inherit an initialised HIP runtime); the workers themselves are forked from
+    # it only after the GPU timing -- a pool of 256 idle workers alive during the timed steps slowed
+    # config E from 44.8 to 50.0 ms per step (profiles/r3/cpu_pool_effect.txt)
+    cpu_ctx, cpu_pool, cpu_cores, npool = None, None, 1, 1
     cores_avail, cores_aff, cores_quota = cpu_core_count()
     if int(os.environ.get("RANK", "0")) == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_cores != 1:
         try:
             import multiprocessing as mp
+            from multiprocessing import forkserver
 
             cpu_cores = max(1, min(args.cpu_cores or cores_avail, cores_aff))
             # one pool of every affinity core: the CPU-share run uses cpu_cores of its workers, the
             # all-affinity run all of them (BASELINE.md §2 asks for the all-cores figure)
             npool = cores_aff if (args.cpu_all_affinity and not args.cpu_cores) else cpu_cores
             if npool > 1:
-                cpu_pool = mp.get_context("forkserver").Pool(npool)
+                cpu_ctx = mp.get_context("forkserver")
+                forkserver.ensure_running()
         except Exception as e:  # the baseline is a reported figure: never fail the bench line for it
             log(f"[bench] multi-core CPU baseline disabled: {e}")
-            cpu_pool, cpu_cores = None, 1
+            cpu_ctx, cpu_cores = None, 1
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # one GPU per rank; FEMASM_DIST_BACKEND=gloo rehearses N > 1 with ranks sharing the visible GPUs
@@ -467,6 +471,12 @@ def main():
     compute_bound = compute_bound and tflops_exec is not None
 
     cpu = None
+    if cpu_ctx is not None:
+        try:
+            cpu_pool = cpu_ctx.Pool(npool)
+        except Exception as e:
+            log(f"[bench] multi-core CPU baseline disabled: {e}")
+            cpu_pool, cpu_cores = None, 1
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         v, nc, t = cpu_baseline(args.cpu_sample_n, args.cpu_reps)
         cpu = {"value": round(v, 4), "unit": "Melements/s", "cores": 1, "kind": "port", "value_1core": round(v, 4),
@@ -556,7 +566,9 @@ def main():
                          "traffic_GBps": None if traffic_gbps is None else round(traffic_gbps, 1),
                          "traffic_frac": None if traffic_gbps is None else round(fracs["traffic_frac"], 4),
                          "traffic_source": tsrc,
-                         "kernel": "k_cell_records + k_gather (row-gather assembly launch)",
+                         "mfma_busy": None if trec is None else trec.get("mfma_busy"),
+                         "kernel": "the assembly launch: per-cell records (or the MFMA element kernel of non-affine "
+                                   "hexahedra) + the row gather + the bc diagonal",
                          "launch_ms": round(launch_ms, 4),
                          "algorithmic_bytes": comp["total"],
                          "algorithmic_bytes_per_cell": round(comp["total"] / ncells_local, 1),

@@ -105,3 +105,26 @@ def test_lifting_matches_oracle(oracle, dev, ct, p, n):
                                _np(marker), _np(gv), x0=_np(a.u), alpha=-1.0, u=_np(a.u), kind=2)
     assert np.abs(ref).max() > 0
     assert np.abs(_np(b) - ref).max() <= RTOL * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("ct,p,n", [(3, 2, (4, 3)), (-4, 1, (2, 3, 2)), (-4, 2, (3, 2, 3))])
+@pytest.mark.parametrize("neo_m,slot_order", [("1", "pos"), ("0", "pos"), ("1", "0")])
+def test_neohookean_gather_paths(oracle, dev, monkeypatch, ct, p, n, neo_m, slot_order):
+    """Both neo-Hookean gathers against the oracle with Dirichlet rows: k_gather_neo (M records, the
+    default; FEMASM_NEO_M=1) and k_gather's items (FEMASM_NEO_M=0), and a plan without the positional
+    order (FEMASM_SLOT_ORDER=0), on which fa_assemble_matrix falls back to k_gather's items."""
+    from femasm import fem
+
+    monkeypatch.setenv("FEMASM_NEO_M", neo_m)
+    monkeypatch.setenv("FEMASM_SLOT_ORDER", slot_order)
+    m, V, a = _setup(oracle, ct, p, n, dev)
+    left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
+    right = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.ones_like(x[0])))
+    bcs = [fem.dirichletbc(0.0, left, V), fem.dirichletbc([0.01] + [0.0] * (m.gdim - 1), right, V)]
+    A = fem.assemble_matrix(a, bcs=bcs)
+    marker, _ = fem._combine_bcs(V, bcs)
+    indptr, indices = oracle.sparsity(_np(V.dofmap), V.num_nodes)
+    lam, mu = oracle.lame(_np(a.E), 0.3)
+    ref = oracle.assemble_neohookean(ct, p, _np(V.dofmap), _np(m.cells), _np(m.x), lam, mu, _np(a.u), indptr, indices,
+                                     bc=_np(marker))
+    assert np.abs(_np(A.data) - ref).max() <= RTOL * np.abs(ref).max()

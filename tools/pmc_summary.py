@@ -25,7 +25,10 @@ for k, d in acc.items():
         print(f"  {c:24s} {mean:16.1f}{extra}  [{len(per)} dispatches]")
 
 
-def counter_total(name, kernels=("k_gather", "k_cell_records")):
+LAUNCH_KERNELS = ("k_gather", "k_cell_records", "k_neo_records", "k_hex_mfma", "k_bc_diag")  # one assembly launch
+
+
+def counter_total(name, kernels=LAUNCH_KERNELS):
     """Sum over the launch's kernels of the per-dispatch mean of one counter, or None if not collected."""
     tot, seen = 0.0, False
     for k, d in acc.items():
@@ -39,7 +42,7 @@ def counter_total(name, kernels=("k_gather", "k_cell_records")):
     return tot if seen else None
 
 
-def traffic_record(root, kernels=("k_gather", "k_cell_records")):
+def traffic_record(root, kernels=LAUNCH_KERNELS):
     """HBM bytes per assembly launch: sum over the launch's kernels of FETCH_SIZE x 2 + WRITE_SIZE (KB)."""
     tot = 0.0
     for k, d in acc.items():
@@ -74,4 +77,14 @@ if len(sys.argv) > 3:  # pmc_summary.py ROOT KEY OUT_JSON: record traffic for be
         # sum of the SQ_INSTS_VALU_*_F64 counters); x 64 lanes = the FP64 work issued to the VALU
         data[key]["fp64_flops"] = 64.0 * fl
         data[key]["fp64_flops_what"] = "64 x SQ_INSTS_VALU_FLOPS_FP64 (lane slots of the issued FP64 VALU instructions)"
+    mb = counter_total("SQ_VALU_MFMA_BUSY_CYCLES", ("k_hex_mfma",))
+    ga = counter_total("GRBM_GUI_ACTIVE", ("k_hex_mfma",))
+    if mb is not None and ga:
+        # MFMA-busy cycles summed over the SIMDs / (the kernel's cycles per XCD x 1024 SIMDs)
+        data[key]["mfma_busy"] = {"busy_cycles": mb, "gui_active": ga, "frac": mb / (ga / 8.0 * 1024.0),
+                                  "kernel": "k_hex_mfma",
+                                  "what": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)"}
+        mops = counter_total("SQ_INSTS_VALU_MFMA_MOPS_F64", ("k_hex_mfma",))
+        if mops is not None:
+            data[key]["mfma_busy"]["mfma_fp64_flops"] = 512.0 * mops  # rocprofv3's MfmaFlopsF64
     json.dump(data, open(out, "w"), indent=1)

@@ -13,6 +13,8 @@ passes=(
   "SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_FLAT"
   "SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64"
 )
+# MFMA busy (k_hex_mfma configs): PASS_MFMA=1 adds the pass
+[ "${PASS_MFMA:-0}" = 1 ] && passes+=("SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE")
 i=0
 for p in "${passes[@]}"; do
   timeout -s KILL 300 rocprofv3 --kernel-include-regex "$kre" --pmc $p -d "$out/pass$i" -o run --output-format csv -- "$@" > "$out/pass$i.log" 2>&1 || { echo "pass $i failed rc=$?"; exit 1; }
