@@ -1260,6 +1260,7 @@ struct GatherArgs {
   const double* lat;  // MAT_AFFT: node lattice codes a0 + 8 a1 + 64 a2
   const double* rec;  // [ncells][Rec::SIZE]
   const uint32_t* bcmask;  // [ncells] or NULL
+  const uint8_t* nodemask; // fused P1 records (k_gather_lin FUSE): [nnodes] constrained-dof bits, or NULL
   int* err;
   // contribution plan (fa_plan_contrib, k_gather_own) or NULL
   const int64_t* cw;       // [nchunks + 1] offsets of the chunks' word sections (u16 units)
@@ -3069,6 +3070,9 @@ __device__ __forceinline__ void chunk_drain(double* acc, int h, int nv, double* 
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rs,
                                         (tid == (jt % NT) && tail_half && !(jt == 0 && h)) ? 8 * (h + nv - 1) : OOB, 0, AUX);
 }
+#ifndef FA_LIN_FUSE
+#define FA_LIN_FUSE 1  // P1 simplices (fa_assemble_matrix): records formed inside k_gather_lin
+#endif
 #ifndef FA_LIN_P1GRAD
 #define FA_LIN_P1GRAD 1  // P1 simplices: blocks from the gradients in the record, no table (k_gather_lin)
 #endif
@@ -3078,7 +3082,7 @@ __device__ __forceinline__ void chunk_drain(double* acc, int h, int nv, double* 
 // 5 no item loads (constant records / slots)
 #define FA_LIN_ABL 0
 #endif
-template <int GD, int NN, int NSPLIT, int NT = 256>
+template <int GD, int NN, int NSPLIT, int NT = 256, bool FUSE = false>
 __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32_t* __restrict__ zero32,
                                                         double* __restrict__ dump, int64_t per) {
   using R = Rec<GD, GD + 1, 1, MAT_LINU>;
@@ -3129,8 +3133,28 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     e = min(max(e, (int64_t)0), nent - 1);
     return eadj[e];
   };
-  struct Item { double r[RL]; uint32_t sl[NBG]; uint32_t mask; };
-  auto load_item = [&](const Desc& d, int32_t pflat, Item& it) {
+  // FUSE (P1 simplices, fa_assemble_matrix): no records kernel; an item loads its cell's vertex
+  // coordinates, E and node bc bits (the vertex ids one chunk earlier still) and forms the uniform-nu
+  // record in registers at the start of its chunk: one pipeline stage more (entries three chunks
+  // ahead, vertex ids two, coordinates one), and no 80-B record written and re-read per cell
+  static_assert(!FUSE || NN == GD + 1, "fused records: P1 simplices");
+  constexpr int NV1 = GD + 1;
+  struct Item {
+    double r[RL];
+    double x[FUSE ? NV1 : 1][GD];
+    double E;
+    uint32_t sl[NBG];
+    uint32_t mask;
+  };
+  struct Vid { int32_t v[NV1]; };
+  auto load_vid = [&](int32_t pflat) -> Vid {
+    Vid w;
+    const int32_t* g = P.M.geom + (int64_t)(pflat / NN) * NV1;
+#pragma unroll
+    for (int t = 0; t < NV1; ++t) w.v[t] = g[t];
+    return w;
+  };
+  auto load_item = [&](const Desc& d, int32_t pflat, Item& it, const Vid& vd) {
     const int64_t c = pflat / NN;
 #if FA_LIN_ABL == 5
 #pragma unroll
@@ -3141,12 +3165,24 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     it.mask = 0u;
     return;
 #endif
-    const dv2* rp = reinterpret_cast<const dv2*>(P.rec + c * RL);
+    if constexpr (FUSE) {
+      uint32_t m = 0u;
 #pragma unroll
-    for (int k = 0; k < RL / 2; ++k) {
-      const dv2 v = rp[k];
-      it.r[2 * k] = v.x;
-      it.r[2 * k + 1] = v.y;
+      for (int t = 0; t < NV1; ++t) {
+#pragma unroll
+        for (int i = 0; i < GD; ++i) it.x[t][i] = P.M.x[(int64_t)vd.v[t] * GD + i];
+        m |= (uint32_t)P.nodemask[(int64_t)vd.v[t] * mkmul] << (t * GD);  // no bcs: P.nodemask[0] of a zero line
+      }
+      it.E = P.F.E[c];
+      it.mask = m * mkmul;
+    } else {
+      const dv2* rp = reinterpret_cast<const dv2*>(P.rec + c * RL);
+#pragma unroll
+      for (int k = 0; k < RL / 2; ++k) {
+        const dv2 v = rp[k];
+        it.r[2 * k] = v.x;
+        it.r[2 * k + 1] = v.y;
+      }
     }
     const int na = (int)(d.a1 - d.a0);
     int64_t e = d.a0 + min(jit, max(na - 1, 0));
@@ -3154,13 +3190,40 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     const uint16_t* sp = P.slots + e * NN + part * NBG;
 #pragma unroll
     for (int bb = 0; bb < NBG; ++bb) it.sl[bb] = sp[bb];
-    it.mask = mk[c * mkmul] * mkmul;
+    if constexpr (!FUSE) it.mask = mk[c * mkmul] * mkmul;
+  };
+  // FUSE: the record (s Ji, sign of mu |J|) of the item's cell from its vertices (cell_record's
+  // MAT_LINU branch on registers)
+  auto form_record = [&](Item& it) {
+    if constexpr (FUSE) {
+      double J[GD][GD], Ji[GD][GD];
+#pragma unroll
+      for (int kk = 0; kk < GD; ++kk)
+#pragma unroll
+        for (int i = 0; i < GD; ++i) J[i][kk] = it.x[kk + 1][i] - it.x[0][i];
+      const double det = jac_inv<GD>(J, Ji);
+      const double mu = it.E / (2.0 * (1.0 + P.F.nu));
+      const double s2 = mu * fabs(det);
+      const double sc = sqrt(fabs(s2));
+#pragma unroll
+      for (int i = 0; i < GD; ++i)
+#pragma unroll
+        for (int kk = 0; kk < GD; ++kk) it.r[i * GD + kk] = sc * Ji[i][kk];
+      it.r[GD * GD] = s2 < 0.0 ? -1.0 : 1.0;
+    }
   };
 
-  Desc d0 = desc(0), d1 = desc(1), d2 = desc(2);
-  int32_t pf0 = load_entry(d0), pf1 = load_entry(d1);
+  Desc d0 = desc(0), d1 = desc(1), d2 = desc(2), d3 = desc(3);
+  int32_t pf0 = load_entry(d0), pf1 = load_entry(d1), pf2 = FUSE ? load_entry(d2) : 0;
   Item cur, nxt;
-  load_item(d0, pf0, cur);
+  Vid vid1{}, vid2{};
+  if constexpr (FUSE) {
+    const Vid vid0 = load_vid(pf0);
+    vid1 = load_vid(pf1);
+    load_item(d0, pf0, cur, vid0);
+  } else {
+    load_item(d0, pf0, cur, vid1);
+  }
   int bad = 0;
   // the prologue's loads complete here (a builtin wait: the compiler's wait counting sees it, so the
   // loop's waits are not widened by pending prologue loads merged in at the loop head)
@@ -3168,9 +3231,18 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
   __syncthreads();  // table and accumulator staged
   for (int64_t k = 0; k < cnt; ++k) {
     // L1: chunk k+2's entry ids; L2: chunk k+1's records / slots / masks (before chunk k's stores)
-    const int32_t pf2 = load_entry(d2);
-    load_item(d1, pf1, nxt);
-    const Desc d3 = desc(k + 3);
+    // (FUSE: entries of chunk k+3, vertex ids of chunk k+2, coordinates of chunk k+1)
+    int32_t pfn;
+    if constexpr (FUSE) {
+      pfn = load_entry(d3);
+      vid2 = load_vid(pf2);
+      load_item(d1, pf1, nxt, vid1);
+    } else {
+      pfn = load_entry(d2);
+      load_item(d1, pf1, nxt, vid1);
+    }
+    const Desc d4 = desc(k + (FUSE ? 4 : 3));
+    form_record(cur);
     // items of chunk k
     const int64_t off = (d0.b0 - abase) * BS2;
     const int h = (int)(off & 1);
@@ -3343,9 +3415,18 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     // rotate the pipeline
     d0 = d1;
     d1 = d2;
-    d2 = d3;
-    pf0 = pf1;
-    pf1 = pf2;
+    if constexpr (FUSE) {
+      d2 = d3;
+      d3 = d4;
+      pf0 = pf1;
+      pf1 = pf2;
+      pf2 = pfn;
+      vid1 = vid2;
+    } else {
+      d2 = d4;
+      pf0 = pf1;
+      pf1 = pfn;
+    }
     cur = nxt;
   }
   if (bad) atomicOr(P.err, 1);
@@ -5423,6 +5504,17 @@ struct GatherStage {
 };
 static inline int64_t align256(int64_t b) { return (b + 255) & ~int64_t(255); }
 
+// constrained-dof bits of every node (bit j: dof node * GD + j), for the fused P1 records
+template <int GD>
+__global__ void k_node_bcmask(const int8_t* __restrict__ bc, int64_t nnodes, uint8_t* __restrict__ out) {
+  for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < nnodes; n += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t m = 0u;
+#pragma unroll
+    for (int j = 0; j < GD; ++j) m |= (bc[n * GD + j] ? 1u : 0u) << j;
+    out[n] = (uint8_t)m;
+  }
+}
+
 template <int GD>
 __global__ void k_bhat(const double* __restrict__ ahat, int nblk, double r, double* __restrict__ bhat) {
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nblk; t += gridDim.x * blockDim.x)
@@ -5561,6 +5653,41 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     // fa_assemble_matrix (both stages here) with a plan the M gather cannot run keeps k_gather's items
     if (neo_m_enabled() && (W.mode != GatherStage::FULL || neo_m_plan_ok(P, NSPLIT)))
       return launch_gather_neo<GD, NN, NQ, NSPLIT>(P, bc, s, W);
+  }
+  if constexpr (MAT == MAT_LINU && R::SIMP && NN == GD + 1 && NN % NSPLIT == 0 && FA_LIN_FUSE) {
+    // P1 simplices through fa_assemble_matrix: k_gather_lin forms the records itself (FUSE)
+    constexpr int LNT = lin_threads(GD, NN);
+    if (W.mode == GatherStage::FULL && P.nchunks > 0 && P.F.E && !P.cw && lin_gather_enabled() && P.eadj &&
+        P.slots && P.slot_order == NSPLIT && !P.corder && P.plan_maxadj * NSPLIT <= LNT && P.plan_maxadj >= 0 &&
+        P.plan_maxb <= gather_maxb(false, GD * GD) && P.nchunks < (1ll << 31)) {
+      int rc;
+      uint8_t* nm = nullptr;
+      if (bc) {
+        if ((rc = scratch_alloc((void**)&nm, (size_t)P.M.nnodes, s))) return rc;
+        k_node_bcmask<GD><<<grid_for(P.M.nnodes), 256, 0, s>>>(bc, P.M.nnodes, nm);
+        LAUNCH_CHECK();
+      }
+      P.nodemask = nm;
+      P.bcmask = nm ? reinterpret_cast<const uint32_t*>(nm) : nullptr;  // only "has bcs" is read
+      P.rec = nullptr;
+      const double nu = P.F.nu;
+      P.rlm = 2.0 * nu / (1.0 - 2.0 * nu);
+      P.trc = 1.0 / (1.0 + P.rlm);
+      uint32_t* zero32 = nullptr;
+      double* dump = nullptr;
+      if ((rc = lin_scratch(&zero32, &dump))) return rc;
+      if (!nm) P.nodemask = reinterpret_cast<const uint8_t*>(zero32);  // a valid address (mask scaled by 0)
+      const int64_t grid = gather_grid(k_gather_lin<GD, NN, NSPLIT, LNT, true>, P.nchunks, LNT);
+      const int64_t per = (P.nchunks + grid - 1) / grid;
+      k_gather_lin<GD, NN, NSPLIT, LNT, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, per);
+      LAUNCH_CHECK();
+      if (bc) {
+        k_bc_diag<GD><<<grid_for((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
+        LAUNCH_CHECK();
+        HIP_TRY(hipFreeAsync(nm, s));
+      }
+      return FA_OK;
+    }
   }
   const int64_t nc = P.M.ncells;
   const int64_t rec_bytes = align256((int64_t)sizeof(double) * R::count(nc));
@@ -5885,7 +6012,7 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;
-    P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr;
+    P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr; P.nodemask = nullptr;
     P.affine = (plan->cell_flags & FA_PLAN_AFFINE) != 0;
     P.t1d = T.t1d; P.lat = T.lat;
     set_contrib(P, plan);
