@@ -229,8 +229,12 @@ int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, const fa_adjace
  * rows of `plan` (any sub-window of A: several plans over disjoint row ranges may be run in any
  * order, e.g. a rank's interface planes first, their exchange overlapping the interior rows).
  * `bc` must be the same in both calls. Same semantics per row as fa_assemble_matrix; elements /
- * forms without a gather kernel return FA_E_UNSUPPORTED. (Replaces the same dolfinx call,
- * FEniCSx/mechanic2d/asym_elasto_damage_model.cc:852-857, as fa_assemble_matrix.) */
+ * forms without a gather kernel return FA_E_UNSUPPORTED. Neo-Hookean simplex forms prepare the
+ * records of the M gather (k_gather_neo), whose plans must be positional (fa_plan_gather_form +
+ * fa_plan_slots + fa_plan_order with an entry buffer); fa_gather_rows refuses another plan with
+ * FA_E_ARG unless the process sets FEMASM_NEO_M=0 (fa_assemble_matrix falls back by itself).
+ * (Replaces the same dolfinx call, FEniCSx/mechanic2d/asym_elasto_damage_model.cc:852-857, as
+ * fa_assemble_matrix.) */
 int fa_gather_work_bytes(const fa_mesh* mesh, const fa_form* form, int64_t* bytes);
 int fa_gather_prepare(const fa_mesh* mesh, const fa_form* form, const int8_t* bc, void* work, void* stream);
 int fa_gather_rows(const fa_mesh* mesh, const fa_form* form, const fa_adjacency* adj, const fa_plan* plan,
