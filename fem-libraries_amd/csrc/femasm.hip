@@ -5453,6 +5453,25 @@ static bool gather_dynamic() {
   return !(e && strcmp(e, "static") == 0);
 }
 
+// k_gather_lin's grid: about FA_LIN_CHUNKS_PER_WG chunks per workgroup, never fewer workgroups than
+// are resident. A grid many times the resident count lets the dispatcher balance the chunks' uneven
+// cost across CUs and XCDs: config E 44.5 ms at the resident count (~4,700 chunks per workgroup),
+// 43.7 / 42.8 / 41.7 / 40.3 / 39.5 ms at 2 / 4 / 8 / 32 / 128 times it, 44.6 ms at 1024 times (~5 per
+// workgroup); config C (162 k chunks) best at 4-8 times (1.30 vs 1.34 ms), 1.46 at 32 times.
+// FEMASM_GATHER_GRID_MULT keeps the resident-count grid times its value (measurement knob).
+#ifndef FA_LIN_CHUNKS_PER_WG
+#define FA_LIN_CHUNKS_PER_WG 32
+#endif
+template <typename K>
+static int64_t lin_grid(K kernel, int64_t nchunks, int block) {
+  const int64_t g0 = gather_grid(kernel, nchunks, block);
+  const char* env = getenv("FEMASM_GATHER_GRID_MULT");
+  if ((env && atof(env) > 0) || !gather_dynamic()) return g0;
+  const int64_t per = (nchunks + 7) / 8;
+  const int64_t g = std::max<int64_t>(g0, nchunks / FA_LIN_CHUNKS_PER_WG / 8 * 8);
+  return std::min<int64_t>(std::min<int64_t>(8 * per, g), kMaxBlocks);
+}
+
 static int chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
   int rc;
   if (P.nchunks >= (1ll << 31)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks (>= 2^31)", (long long)P.nchunks);
@@ -5677,7 +5696,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       double* dump = nullptr;
       if ((rc = lin_scratch(&zero32, &dump))) return rc;
       if (!nm) P.nodemask = reinterpret_cast<const uint8_t*>(zero32);  // a valid address (mask scaled by 0)
-      const int64_t grid = gather_grid(k_gather_lin<GD, NN, NSPLIT, LNT, true>, P.nchunks, LNT);
+      const int64_t grid = lin_grid(k_gather_lin<GD, NN, NSPLIT, LNT, true>, P.nchunks, LNT);
       const int64_t per = (P.nchunks + grid - 1) / grid;
       k_gather_lin<GD, NN, NSPLIT, LNT, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, per);
       LAUNCH_CHECK();
@@ -5734,7 +5753,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       uint32_t* zero32 = nullptr;
       double* dump = nullptr;
       if ((rc = lin_scratch(&zero32, &dump))) return rc;
-      const int64_t grid = gather_grid(k_gather_lin<GD, NN, NSPLIT, LNT>, P.nchunks, LNT);
+      const int64_t grid = lin_grid(k_gather_lin<GD, NN, NSPLIT, LNT>, P.nchunks, LNT);
       const int64_t per = (P.nchunks + grid - 1) / grid;
       k_gather_lin<GD, NN, NSPLIT, LNT><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, per);
       LAUNCH_CHECK();
