@@ -5462,13 +5462,18 @@ static bool gather_dynamic() {
 #ifndef FA_LIN_CHUNKS_PER_WG
 #define FA_LIN_CHUNKS_PER_WG 32
 #endif
+// k_gather_neo likewise, at ~FA_NEO_CHUNKS_PER_WG (config E-neo, alternating on one box: 74.0-74.3 ms
+// at 64 times the resident count against 75.5-76.9 at 1 time)
+#ifndef FA_NEO_CHUNKS_PER_WG
+#define FA_NEO_CHUNKS_PER_WG 128
+#endif
 template <typename K>
-static int64_t lin_grid(K kernel, int64_t nchunks, int block) {
+static int64_t lin_grid(K kernel, int64_t nchunks, int block, int per_wg = FA_LIN_CHUNKS_PER_WG) {
   const int64_t g0 = gather_grid(kernel, nchunks, block);
   const char* env = getenv("FEMASM_GATHER_GRID_MULT");
   if ((env && atof(env) > 0) || !gather_dynamic()) return g0;
   const int64_t per = (nchunks + 7) / 8;
-  const int64_t g = std::max<int64_t>(g0, nchunks / FA_LIN_CHUNKS_PER_WG / 8 * 8);
+  const int64_t g = std::max<int64_t>(g0, nchunks / per_wg / 8 * 8);
   return std::min<int64_t>(std::min<int64_t>(8 * per, g), kMaxBlocks);
 }
 
@@ -5620,7 +5625,7 @@ static int launch_gather_neo(GatherArgs P, const int8_t* bc, hipStream_t s, cons
     double* dump = nullptr;
     if ((rc = lin_scratch(&zero32, &dump))) return rc;
     constexpr int QS = neo_qsplit<NQ>();
-    const int64_t grid = gather_grid(k_gather_neo<GD, NN, NQ, NSPLIT, QS>, P.nchunks, 256 * QS);
+    const int64_t grid = lin_grid(k_gather_neo<GD, NN, NQ, NSPLIT, QS>, P.nchunks, 256 * QS, FA_NEO_CHUNKS_PER_WG);
     k_gather_neo<GD, NN, NQ, NSPLIT, QS><<<(unsigned)grid, 256 * QS, 0, s>>>(P, zero32, dump);
     LAUNCH_CHECK();
     if (bc) {  // Dirichlet diagonals (dolfinx set_diagonal) of the plan's rows
