@@ -3368,6 +3368,12 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
             for (int kk = 0; kk < GD; ++kk) ap[i * GD + kk] = o[i * GD + kk] + G[i][kk];
 #elif FA_LIN_ABL == 2
           if (G[0][0] == 1.2345e-300) ap[0] = G[1][1];
+#elif FA_LIN_ABL == 6
+#pragma unroll
+          for (int i = 0; i < GD; ++i)
+#pragma unroll
+            for (int kk = 0; kk < GD; ++kk)
+              atomicAdd(reinterpret_cast<unsigned long long*>(ap + i * GD + kk), __builtin_bit_cast(unsigned long long, G[i][kk]));
 #else
 #pragma unroll
           for (int i = 0; i < GD; ++i)
@@ -3390,9 +3396,11 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     for (int u = 0; u < SW; ++u) v[u] = acc2[h + max(min(tid + NT * u, np - 1), 0)];
     const double hv = acc[h], tv = acc[max(nv - 1, 0) + h];
     __syncthreads();  // B2: every read is done before any zero
+#if FA_LIN_ABL != 7
 #pragma unroll
     for (int u = 0; u < SW; ++u)
       if (tid + NT * u < np) acc2[h + tid + NT * u] = dv2{0.0, 0.0};
+#endif
     // the unpaired head (acc[1] when h = 1) and tail sit in pairs whose other half is never written
     if (tid == 0) acc2[0] = dv2{0.0, 0.0};
     if (tid == 1) acc2[(max(nv - 1, 0) + h) >> 1] = dv2{0.0, 0.0};
@@ -4813,7 +4821,12 @@ __global__ void k_plan_colors_stats(const int64_t* __restrict__ row_start, const
 #ifndef FA_P1TET_NT
 #define FA_P1TET_NT 256  // 512 measured 1.72 vs 1.68 ms on config C
 #endif
-__host__ __device__ constexpr int lin_threads(int gd, int nn) { return gd == 3 && nn == 4 ? FA_P1TET_NT : 256; }
+#ifndef FA_P2TET_NT
+#define FA_P2TET_NT 256
+#endif
+__host__ __device__ constexpr int lin_threads(int gd, int nn) {
+  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : 256;
+}
 static int lin_simplex_nsplit(int ct, int p, int nq, bool affine = false) {
   // affine hexahedra (MAT_AFFT): Q1 / Q2 / Q3 with their default rules
   if (affine && ct == FA_HEXAHEDRON && p == 1 && nq == 8) return 2;

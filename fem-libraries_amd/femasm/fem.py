@@ -359,14 +359,20 @@ def dirichletbc(value, nodes: torch.Tensor, V: FunctionSpace, components=None) -
     return DirichletBC(V, dofs, g)
 
 
-def _bcs_key(V: FunctionSpace, bcs, with_g: bool):
-    # identity + storage + in-place version of every input tensor: an edited bc misses the cache
-    parts = [with_g]
-    for bc in bcs:
-        parts.append((id(bc), bc.dofs.data_ptr(), bc.dofs.numel(), bc.dofs._version))
-        if with_g:
-            parts.append((bc.g.data_ptr(), bc.g._version))
-    return tuple(parts)
+def _bc_state(bc, with_g: bool):
+    # the exact tensor objects a bc holds (weakly) and their in-place versions: a hit needs the same
+    # objects at the same versions, so a reassigned bc.dofs / bc.g (even one the caching allocator
+    # put at a freed tensor's address) or an edited one misses the cache
+    st = [weakref.ref(bc), weakref.ref(bc.dofs), bc.dofs._version]
+    if with_g:
+        st += [weakref.ref(bc.g), bc.g._version]
+    return st
+
+
+def _bc_state_ok(st, bc, with_g: bool) -> bool:
+    if st[0]() is not bc or st[1]() is not bc.dofs or st[2] != bc.dofs._version:
+        return False
+    return not with_g or (st[3]() is bc.g and st[4] == bc.g._version)
 
 
 def _combine_bcs(V: FunctionSpace, bcs, with_g: bool = True):
@@ -376,9 +382,9 @@ def _combine_bcs(V: FunctionSpace, bcs, with_g: bool = True):
     if not bcs:
         return None, None
     cache = V.__dict__.setdefault("_bc_cache", {})
-    key = _bcs_key(V, bcs, with_g)
+    key = (with_g,) + tuple(id(bc) for bc in bcs)
     hit = cache.get(key)
-    if hit is not None and all(w() is bc for w, bc in zip(hit[2], bcs)):
+    if hit is not None and all(_bc_state_ok(st, bc, with_g) for st, bc in zip(hit[2], bcs)):
         return hit[0], hit[1]
     marker = torch.zeros(V.num_dofs, dtype=torch.int8, device=V.mesh.device)
     g = torch.zeros(V.num_dofs, dtype=torch.float64, device=V.mesh.device) if with_g else None
@@ -386,11 +392,12 @@ def _combine_bcs(V: FunctionSpace, bcs, with_g: bool = True):
         marker[bc.dofs] = 1
         if with_g:
             g[bc.dofs] = bc.g[bc.dofs]
+    cache.pop(key, None)
     if len(cache) >= 8:  # a handful of bcs sets per space; drop the oldest
         cache.pop(next(iter(cache)))
-    # weak references (a bc refers to V: strong ones would make a cycle that keeps V's tensors alive
-    # until a GC pass); a hit is checked against them, so a reused id of a dead bc cannot match
-    cache[key] = (marker, g, [weakref.ref(bc) for bc in bcs])
+    # weak references only (a bc refers to V: strong ones would make a cycle that keeps V's tensors
+    # alive until a GC pass); a hit is checked against them, so a reused id cannot match
+    cache[key] = (marker, g, [_bc_state(bc, with_g) for bc in bcs])
     return marker, g
 
 

@@ -33,6 +33,8 @@ def _worker(rank, world, port, n, kind="linear"):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
     from femasm import fem, parallel
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import rowparity
 
     dev = torch.device("cuda", 0)
     prob = parallel.SlabProblem(n, rank, world, dev, form=kind)
@@ -48,8 +50,7 @@ def _worker(rank, world, port, n, kind="linear"):
     ix_g = A.indices.cpu().numpy()
     vg = A.data.cpu().numpy()
     w0 = ip_l[part.row_begin]
-    scale = np.abs(vg).max()
-    err = 0.0
+    got, ref, ptr = [], [], [0]
     for r in range(part.row_begin, part.row_end):
         g = r + part.node_offset
         lc = ix_l[ip_l[r]:ip_l[r + 1]]
@@ -60,8 +61,11 @@ def _worker(rank, world, port, n, kind="linear"):
                 continue  # the rank's own partial sums, sent to the owner
             keep = lc >= part.lower[0]  # suffix all-reduce: the exchanged blocks only
             lv, gv = lv[keep], gv[keep]
-        err = max(err, float(np.abs(lv - gv).max()))
-    assert err <= 1e-12 * scale, f"rank {rank}: rel err {err / scale:.2e}"
+        got.append(lv)
+        ref.append(gv)
+        ptr.append(ptr[-1] + len(lv))
+    # per scalar row, each row held to its own scale (tests/rowparity.py)
+    rowparity.assert_rows_close(np.concatenate(got), np.concatenate(ref), np.array(ptr), what=f"rank {rank}:")
     dist.destroy_process_group()
 
 
@@ -128,12 +132,13 @@ def test_slab_ghost_mode_gpu(world, n, kind):
     sys.path.insert(0, os.path.join(ROOT, "fem-libraries_amd"))
     import bench
     from femasm import fem, parallel
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import rowparity
 
     dev = torch.device("cuda", 0)
     m, V, a, bcs = bench.build_problem(n, dev, cfg=bench.CONFIGS["Eneo" if kind == "neo" else "E"])
     A = fem.assemble_matrix(a, bcs=bcs)
     ip_g, ix_g, vg = A.indptr.cpu().numpy(), A.indices.cpu().numpy(), A.data.cpu().numpy()
-    scale = np.abs(vg).max()
     for rank in range(world):
         prob = parallel.SlabProblem(n, rank, world, dev, form=kind, mode="ghost")
         prob.assemble()
@@ -144,8 +149,10 @@ def test_slab_ghost_mode_gpu(world, n, kind):
         ip_l, ix_l = prob.A.indptr.cpu().numpy(), prob.A.indices.cpu().numpy()
         vl = prob.A.parts[0][2].cpu().numpy()
         w0 = ip_l[r0]
+        g0, g1 = r0 + part.node_offset, r1 + part.node_offset
         for r in range(r0, r1):
             g = r + part.node_offset
             assert np.array_equal(ix_l[ip_l[r]:ip_l[r + 1]] + part.node_offset, ix_g[ip_g[g]:ip_g[g + 1]])
-            err = np.abs(vl[ip_l[r] - w0:ip_l[r + 1] - w0] - vg[ip_g[g]:ip_g[g + 1]]).max()
-            assert err <= 1e-12 * scale, f"rank {rank} row {r}: rel err {err / scale:.2e}"
+        # owned rows are one contiguous value range on both sides: per-row parity over it
+        rowparity.assert_rows_close(vl[ip_l[r0] - w0:ip_l[r1] - w0], vg[ip_g[g0]:ip_g[g1]], ip_l[r0:r1 + 1] - ip_l[r0],
+                                    what=f"rank {rank}:")

@@ -51,6 +51,8 @@ def _worker(rank, world, port, n, async_op=False, mode="rows", kind="linear"):
     from femasm import fem, mesh, parallel
     from femasm.materials import e_range
     from oracle import oracle as O
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import rowparity
 
     p, bs, L, ct = 2, 3, (1.0, 1.0, 1.0), mesh.CellType.tetrahedron
     part = parallel.SlabPartition((n, n, n), p, rank, world)
@@ -90,8 +92,7 @@ def _worker(rank, world, port, n, async_op=False, mode="rows", kind="linear"):
     gmarker = _bc_marker(gx, bs).numpy()
     glam, gmu = O.lame(e_range()[np.arange(m.num_cells) % 200], 0.3)
     gvals = _assemble(O, kind, p, dof, m.cells.numpy(), m.x.numpy(), glam, gmu, _state(gx, kind), gip, gix, gmarker)
-    scale = np.abs(gvals).max()
-    err = 0.0
+    got, ref, ptr = [], [], [0]
     for r in range(part.row_begin, part.row_end):  # owned rows and the ghost copy of the lower interface
         g = r + part.node_offset
         lc = indices[indptr[r]:indptr[r + 1]] + part.node_offset
@@ -105,8 +106,11 @@ def _worker(rank, world, port, n, async_op=False, mode="rows", kind="linear"):
             if mode == "suffix":
                 keep = lc >= part.lower[0] + part.node_offset  # non-owned copy: the exchanged blocks only
                 lv, gv = lv[keep], gv[keep]
-        err = max(err, float(np.abs(lv - gv).max()))
-    assert err <= 1e-12 * scale, f"rank {rank}: rel err {err / scale:.2e}"
+        got.append(lv)
+        ref.append(gv)
+        ptr.append(ptr[-1] + len(lv))
+    # per scalar row, each row held to its own scale (tests/rowparity.py)
+    rowparity.assert_rows_close(np.concatenate(got), np.concatenate(ref), np.array(ptr), what=f"rank {rank}:")
     dist.destroy_process_group()
 
 

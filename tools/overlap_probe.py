@@ -1,0 +1,100 @@
+"""Is the N = 8 exchange overlap affordable?
+
+On ONE GPU, for the config-E slab of rank `--rank` of `--world` (side 203, 25-26 of the 203 cube
+layers): time the interior-row gather of SlabProblem (fa_gather_rows over the rows between the two
+interface planes) alone, then again while a device-to-device copy of the HBM footprint of one
+boundary's transfer (the interface suffix the rank sends, ~0.28 GB) runs on a second stream, and the
+same slab's ghost-mode assembly (its layers + the layer above, no exchange). HIP events on the
+stream each kernel runs on. Writes one JSON line.
+
+usage: python tools/overlap_probe.py [--n 203] [--rank 3] [--world 8] [--reps 10]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fem-libraries_amd"))
+
+import torch  # noqa: E402
+
+from femasm.parallel import SlabProblem  # noqa: E402
+
+
+def timed(fn, reps, stream):
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return statistics.median(ts), min(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=203)
+    ap.add_argument("--rank", type=int, default=3)
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--form", default="linear")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    out = {"n": args.n, "rank": args.rank, "world": args.world, "form": args.form}
+    prob = SlabProblem(args.n, args.rank, args.world, dev, groups=[None] * (args.world - 1), form=args.form)
+    sg = prob.split
+    out["cells"] = prob.num_cells
+    out["exchange_bytes_sent"] = prob.exchange_bytes
+    out["exchange_bytes_recv"] = prob.exchange_recv_bytes
+    cur = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+    nbytes = max(prob.exchange_bytes, prob.exchange_recv_bytes)
+    src = torch.empty(nbytes // 8, dtype=torch.float64, device=dev).fill_(1.0)
+    dst = torch.empty_like(src)
+    sg.prepare()
+    for i in range(sg_n := len(sg.plans)):
+        sg.rows(i)
+    torch.cuda.synchronize()
+    inner = prob.n_iface  # the interior range follows the interface planes
+
+    # the copy alone (its own duration on the side stream)
+    def copy():
+        with torch.cuda.stream(side):
+            dst.copy_(src)
+    copy_ms, _ = timed(copy, args.reps, side)
+    out["copy_alone_ms"] = copy_ms
+    out["copy_GBps"] = 2 * nbytes / copy_ms / 1e6
+
+    # full single-rank assembly (records + every range), interior alone, interior + concurrent copy
+    def full():
+        sg.prepare()
+        for i in range(sg_n):
+            sg.rows(i)
+    out["slab_assembly_ms"], _ = timed(full, args.reps, cur)
+    out["interior_alone_ms"], out["interior_alone_min_ms"] = timed(lambda: sg.rows(inner), args.reps, cur)
+
+    def interior_with_copy():
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            dst.copy_(src)
+        sg.rows(inner)
+        cur.wait_stream(side)
+    out["interior_with_copy_ms"], out["interior_with_copy_min_ms"] = timed(interior_with_copy, args.reps, cur)
+    out["overlap_cost_ms"] = out["interior_with_copy_ms"] - out["interior_alone_ms"]
+    del prob, sg
+    torch.cuda.empty_cache()
+    ghost = SlabProblem(args.n, args.rank, args.world, dev, groups=[None] * (args.world - 1), form=args.form,
+                        mode="ghost")
+    ghost.assemble()
+    torch.cuda.synchronize()
+    out["ghost_cells"] = ghost.num_cells_assembled
+    out["ghost_assembly_ms"], _ = timed(ghost.assemble, args.reps, cur)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
