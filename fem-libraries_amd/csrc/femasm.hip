@@ -79,6 +79,7 @@ struct DevTables {
   const double* t1d;   // tensor cells: 1-D matrices S, M, C [3][p+1][p+1] (tensor_1d_mats)
   const double* lat;   // tensor cells: node lattice code a0 + 8 a1 + 64 a2 per node (as doubles)
   int ndoubles;
+  double amax;         // simplex: max |ahat| entry (bounds the blocks of the fixed-point gather)
 };
 
 static std::mutex g_tab_mu;
@@ -107,6 +108,7 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
   h.insert(h.end(), T.gphi.begin(), T.gphi.end());
   // reference tensor of grad-grad products (affine simplices: G_ab = |J| Ji^T Ahat_ab Ji)
   const size_t off_ahat = h.size();
+  double amax = 0.0;
   if (is_simplex(ct)) {
     for (int a = 0; a < T.nn; ++a)
       for (int b = 0; b < T.nn; ++b)
@@ -116,6 +118,7 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
             for (int q = 0; q < T.nq; ++q)
               v += T.wq[q] * T.dphi[((size_t)q * T.nn + a) * T.td + i] * T.dphi[((size_t)q * T.nn + b) * T.td + j];
             h.push_back(v);
+            amax = std::max(amax, std::fabs(v));
           }
   }
   // tensor cells: 1-D matrices of the affine fast path and the node lattice codes
@@ -143,6 +146,7 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
   D.t1d = is_simplex(ct) ? nullptr : d + off_t1d;
   D.lat = is_simplex(ct) ? nullptr : d + off_lat;
   D.ndoubles = (int)h.size();
+  D.amax = amax;
   g_tabs[key] = D;
   *out = D;
   return FA_OK;
@@ -833,16 +837,9 @@ typedef double fa_d4 __attribute__((ext_vector_type(4)));
 // the 256 VGPRs of 2 waves / SIMD (16 waves of one tile were capped at 128 VGPRs and spilled 35)
 __host__ __device__ constexpr int hex_tpw(int nn) { return ((nn + 15) / 16) * ((nn + 15) / 16) >= 16 ? 2 : 1; }
 __host__ __device__ constexpr int hex_threads(int nn) { return 64 * ((nn + 15) / 16) * ((nn + 15) / 16) / hex_tpw(nn); }
-// MODE 2 (block store for the row gather) computes the upper-triangle tiles only (ta <= tb: 10 of 16
-// for Q3) and stores each off-diagonal tile twice, as itself and transposed (K_ba = K_ab^T: M_ik[a][b]
-// = Phi_i[a] . Phi_k[b] = M_ki[b][a]); FA_HEX_UPPER=0 computes every tile
-#ifndef FA_HEX_UPPER
-#define FA_HEX_UPPER 0  // 1 measured slower on config Dmfma: k_hex_mfma 27.5 -> 38.5 ms (5-wave workgroups at
-                        // 2 waves / SIMD leave 3 of a CU's 8 wave slots idle; transposed stores of 288-B runs)
-#endif
-__host__ __device__ constexpr int hex_ntiles(int nn, int mode) {
-  return (mode == 2 && FA_HEX_UPPER) ? ((nn + 15) / 16) * ((nn + 15) / 16 + 1) / 2 : ((nn + 15) / 16) * ((nn + 15) / 16);
-}
+// every (a, b) tile is computed (the upper triangle with transposed stores measured slower on config
+// Dmfma: 38.5 vs 27.5 ms, 5-wave workgroups at 2 waves / SIMD leave 3 of a CU's 8 wave slots idle)
+__host__ __device__ constexpr int hex_ntiles(int nn, int mode) { return ((nn + 15) / 16) * ((nn + 15) / 16); }
 __host__ __device__ constexpr int hex_threads_m(int nn, int mode) {
   return 64 * ((hex_ntiles(nn, mode) + hex_tpw(nn) - 1) / hex_tpw(nn));
 }
@@ -852,21 +849,13 @@ __global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
     MeshView M, FormView F, DevTables T, int64_t c0, int64_t ncells, double* __restrict__ Ae, BsrView A,
     const int8_t* __restrict__ bc, int* __restrict__ err) {
   constexpr int NT = (NN + 15) / 16;  // 16-row tiles per side; TPW (a, b) tiles per wave
-  constexpr bool UPPER = MODE == 2 && FA_HEX_UPPER;
   constexpr int NTL = hex_ntiles(NN, MODE);  // tiles computed
   constexpr int TPW = hex_tpw(NN), NWAVE = (NTL + TPW - 1) / TPW;
   constexpr int NTHR = hex_threads_m(NN, MODE);
-  // tile t -> (ta, tb): row-major over the full grid, or over the upper triangle (UPPER)
+  // tile t -> (ta, tb): row-major over the grid
   auto tile_of = [](int t, int& ta, int& tb) {
-    if constexpr (UPPER) {
-      int r = 0, rem = t < NTL ? t : NTL - 1;
-      while (rem >= NT - r) { rem -= NT - r; ++r; }
-      ta = r;
-      tb = r + rem;
-    } else {
-      ta = t / NT;
-      tb = t % NT;
-    }
+    ta = t / NT;
+    tb = t % NT;
   };
   constexpr int NNP = NT * 16 + 16;   // row stride: +16 doubles puts q and q+1 on opposite bank halves
   constexpr int QMAX = (NQ + 3) & ~3;
@@ -989,32 +978,6 @@ __global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          if (UPPER && ta != tb) {
-            // the transposed tile: block (b, a) = K_ab^T; row b holds the 4 blocks a = ta*16 + 4r + {0..3}
-            if (a < NN && b < NN) {
-              const double tr = acc[0][r] + acc[4][r] + acc[8][r];
-              const uint32_t rm = s_bcn[a], cm = s_bcn[b];
-#pragma unroll
-              for (int i = 0; i < 3; ++i)
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                  const double v = lam * acc[i * 3 + k][r] + mu * acc[k * 3 + i][r] + (i == k ? mu * tr : 0.0);
-                  st[(lane & 15) * 36 + (lane >> 4) * 9 + k * 3 + i] = (((rm >> i) | (cm >> k)) & 1u) ? 0.0 : v;
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const int nav = min(4, NN - (ta * 16 + 4 * r)) * 9;  // valid values of a row run
-            for (int t = lane; t < 16 * 36; t += 64) {
-              const int j = t / 36, off = t - j * 36;
-              const int bj = tb * 16 + j;
-              if (bj < NN && off < nav) Ae[((ci * NN + bj) * NN + ta * 16 + 4 * r) * 9 + off] = st[t];
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          }
         }
         continue;
       }
@@ -1121,24 +1084,17 @@ __global__ void k_bc_diag(BsrView A, int64_t nnodes, const int8_t* __restrict__ 
 //     contiguous so its L2 holds the cells they share). Items (adjacency entry, column group)
 //     read one record + the column node ids, build 3x3 blocks in registers and add them into
 //     the LDS copy of the chunk; the chunk is then stored with coalesced plain stores.
-#ifndef FA_GATHER_LDS
-#define FA_GATHER_LDS 32768  // 4 workgroups / CU with k_gather_lin's table (E: 44.3 vs 45.3 ms at 28672)
-#endif
+constexpr int FA_GATHER_LDS = 32768;  // 4 workgroups / CU with k_gather_lin's table (E: 44.3 vs 45.3 ms at 28672)
 static constexpr int kGatherLdsValues = FA_GATHER_LDS;  // accumulator bytes per workgroup (4 WG / CU)
 // neo-Hookean gather (2 workgroups / CU, VGPR-bound): a larger accumulator, and chunks capped at
 // 256 / NSPLIT adjacency entries so one chunk's items fill the workgroup's 256 lanes once
 // (fa_plan_gather_form); with the default plan ~96 entries -> 192 items left a wave idle
-#ifndef FA_GATHER_LDS_NEO
-#define FA_GATHER_LDS_NEO 46080
-#endif
+constexpr int FA_GATHER_LDS_NEO = 46080;
 static constexpr int kGatherLdsNeo = FA_GATHER_LDS_NEO;
-#ifndef FA_NEO_NSPLIT
-#define FA_NEO_NSPLIT 2  // column items of 5 columns; see dispatch_gather
-#endif
+constexpr int FA_NEO_NSPLIT = 2;  // neo-Hookean column items of 5 columns (E-neo at 2 waves / SIMD, round 2: NSPLIT 2
+                                  // 342 ms, 5 at 3 waves 349, 10 at 4 waves 461)
 static constexpr int kGatherNeoEntries = 256 / FA_NEO_NSPLIT;
-#ifndef FA_GATHER_ENTRY_CAP
-#define FA_GATHER_ENTRY_CAP 512  // adjacency entries per chunk of the default plan (512 = the LDS arrays' cap)
-#endif
+constexpr int FA_GATHER_ENTRY_CAP = 512;  // adjacency entries per chunk of the default plan (512 = the LDS arrays' cap)
 // blocks of the accumulator of a gather kernel (the plan's chunks must fit it)
 __host__ __device__ constexpr int gather_maxb(bool neo, int bs2) {
   return (neo ? kGatherLdsNeo : kGatherLdsValues) / (8 * bs2) < 1023 ? (neo ? kGatherLdsNeo : kGatherLdsValues) / (8 * bs2)
@@ -1150,12 +1106,9 @@ static constexpr int kGatherMaxRows = 128;      // rows per chunk
 // gather variant whose blocks come from a per-cell block store [cell][a][b][GD][GD] (hexahedra:
 // written by the MFMA kernel) instead of being computed from a record
 constexpr int MAT_BLOCKS = 9;
-#ifndef FA_EB_WAVE
-#define FA_EB_WAVE 1  // MAT_BLOCKS: one wave per adjacency entry (coalesced block-store reads), 0: lane items
-#endif
-#ifndef FA_EB_UNROLL
-#define FA_EB_UNROLL 2
-#endif
+// MAT_BLOCKS: adjacency entries in flight per wave (one wave per entry, coalesced block-store reads):
+// measured 1 / 2 / 3 -> Dmfma 50.0 / 46.0 / 47.3 ms
+constexpr int kEbUnroll = 2;
 // linear elasticity with one Poisson ratio for all cells (E per cell): lam / mu = r is uniform, so
 // lam G + mu G^T = mu |J| Ji^T (r Ahat + Ahat^T) Ji; the record holds s Ji with s^2 = mu |J|
 // (and the sign of mu |J|), the table B_ab = r Ahat_ab + Ahat_ab^T, and
@@ -1167,67 +1120,19 @@ constexpr int MAT_LINU = 10;
 // gather for Q1-Q3 hexahedra of a structured mesh, with no element-matrix store
 constexpr int MAT_AFFT = 11;
 
-#ifndef FA_NEO_INV
-#define FA_NEO_INV 1  // neo-Hookean records: AD of the strain energy in its invariants (F + 5 scalars per
-                      // point) instead of the 45-entry AD tangent per point
-#endif
-#ifndef FA_NEO_CREC
-// invariant records hold C = cof F and {W_JJ + W_J/J, W_J/J, 2 W_1} (12 doubles per point in 3-D)
-// instead of F and all five coefficients (14): the reference potential W = mu/2 (I1 - 3) - mu ln J
-// + lam/2 (ln J)^2 is linear in I1, so W_11 = W_1J = 0 and the F F^T / F C^T terms of the tangent
-// vanish identically; the gather then needs neither F nor the per-point cofactor
-#define FA_NEO_CREC 1
-#endif
-#ifndef FA_NEO_TILE
-#define FA_NEO_TILE 1  // neo-Hookean C records in 64-cell tiles (Rec::TILED)
-#endif
-#ifndef FA_NEO_SREC
-// tiled C records with the cofactor scaled: W_JJ + W_J/J = lam / J^2 has the sign s_c of the cell's
-// lam at every point and 2 W_1 = mu is constant, so a point needs only C' = sqrt|c2| C and
-// rho = c3 / |c2| (10 doubles instead of 12), the head s_c and mu: K_ab += s_c C'ga (C'gb)^T -
-// rho C'gb (C'ga)^T + mu (ga.gb) I (lam = 0: C' = C, s_c = 0, rho = c3)
-#define FA_NEO_SREC 1
-#endif
-#ifndef FA_REC_STAGED
-#define FA_REC_STAGED 1  // small records stored through LDS as contiguous runs (k_cell_records_staged)
-#endif
 template <int GD, int NV, int NQ, int MAT>
 struct Rec {
   static constexpr bool SIMP = (NV == GD + 1) || MAT == MAT_AFFT;  // affine: one Jacobian per cell
-  static constexpr int N = GD * GD;
-  static constexpr int NTRI = N * (N + 1) / 2;  // stored upper triangle of the tangent
-  // LIN simplex: Ji[GD*GD], wdet, lam, mu | LINU (simplex): s Ji[GD*GD], sign(mu wdet) | LIN tensor: NQ x (Ji[GD*GD], wdet), lam, mu |
-  // DAMAGE (P1 tri): g[3][2], w, H[3][3] | NEO (simplex): Ji[GD*GD], wdet, NQ x A_q upper triangle
-  // NEO per quadrature point (FA_NEO_INV): F[GD*GD] and the strain-energy coefficients s11, s1J,
-  // sCC, sCt, s1 (neo_energy_coeffs) from QOFF, stride QSTR; FA_NEO_INV=0: the 45-entry upper
-  // triangle of dP/dF at N + 1, stride NTRI
-  static constexpr bool SREC = MAT == FA_NEO_HOOKEAN && FA_NEO_INV && FA_NEO_CREC && FA_NEO_TILE && FA_NEO_SREC;
-  // SREC head: J^-1, |J|, s_c, mu | point: C' (N), rho
-  static constexpr int QOFF = SREC ? ((N + 4) & ~1) : (FA_NEO_INV ? ((N + 2) & ~1) : N + 1);
-  static constexpr int QSTR = SREC ? ((N + 2) & ~1) : (FA_NEO_INV ? (FA_NEO_CREC ? ((N + 4) & ~1) : ((N + 6) & ~1)) : NTRI);
+  // LIN simplex: Ji[GD*GD], wdet, lam, mu | LINU (simplex): s Ji[GD*GD], sign(mu wdet) |
+  // LIN tensor: NQ x (Ji[GD*GD], wdet), lam, mu | DAMAGE (P1 tri): g[3][2], w, H[3][3]
   static constexpr int RAW = MAT == MAT_BLOCKS ? 2
                              : (MAT == MAT_LINU || MAT == MAT_AFFT) ? GD * GD + 1
                              : MAT == FA_ASYM_DAMAGE ? 16
-                             : MAT == FA_NEO_HOOKEAN ? QOFF + NQ * QSTR
                                                      : (SIMP ? GD * GD + 3 : NQ * (GD * GD + 1) + 2);
   static constexpr int SIZE = (RAW + 1) & ~1;  // even: 16-byte aligned records
-  // neo-Hookean C records (FA_NEO_TILE): tiles of 64 cells, [64 heads][NQ][64 point records], so
-  // the records kernel stores every block of a tile contiguously (k_neo_records_tiled); a cell's
-  // head and each of its point records stay contiguous and 16-B aligned for the gather's loads
-  static constexpr bool TILED = MAT == FA_NEO_HOOKEAN && FA_NEO_INV && FA_NEO_CREC && FA_NEO_TILE;
-  static constexpr int PSTR = TILED ? 64 * QSTR : QSTR;  // stride between a cell's point records
-  __host__ __device__ static constexpr int64_t head(int64_t c) {
-    return TILED ? (c >> 6) * (64 * SIZE) + (c & 63) * QOFF : c * SIZE;
-  }
-  __host__ __device__ static constexpr int64_t point0(int64_t c) {
-    return TILED ? (c >> 6) * (64 * SIZE) + 64 * QOFF + (c & 63) * QSTR : c * SIZE + QOFF;
-  }
-  __host__ __device__ static constexpr int64_t count(int64_t nc) { return TILED ? (nc + 63) / 64 * 64 * SIZE : nc * SIZE; }
+  __host__ __device__ static constexpr int64_t head(int64_t c) { return c * SIZE; }
+  __host__ __device__ static constexpr int64_t count(int64_t nc) { return nc * SIZE; }
 };
-
-__host__ __device__ constexpr int tri_index(int i, int j, int n) {  // upper triangle, i <= j
-  return i * n - i * (i - 1) / 2 + (j - i);
-}
 
 struct GatherArgs {
   MeshView M;
@@ -1262,6 +1167,12 @@ struct GatherArgs {
   const uint32_t* bcmask;  // [ncells] or NULL
   const uint8_t* nodemask; // fused P1 records (k_gather_lin FUSE): [nnodes] constrained-dof bits, or NULL
   int* err;
+  // deterministic assembly (FA_DETERMINISTIC): k_gather_lin accumulates 64-bit fixed point (integer
+  // LDS atomics, order-independent sums); fixc bounds an item's block entries by fixc * rho^2,
+  // rho = sum |record entries|
+  int fix;
+  double fixc;
+  double amax;  // max |ahat| entry of the element (DevTables::amax)
   // contribution plan (fa_plan_contrib, k_gather_own) or NULL
   const int64_t* cw;       // [nchunks + 1] offsets of the chunks' word sections (u16 units)
   const int32_t* ccells;   // [nchunks][FA_OWN_CCAP] the chunk's distinct cells (-1 padded)
@@ -1363,68 +1274,7 @@ __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, co
                                                       uint32_t* __restrict__ bcmask) {
   using R = Rec<GD, NV, NQ, MAT>;
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < M.ncells; c += (int64_t)gridDim.x * blockDim.x) {
-  if constexpr (MAT == FA_NEO_HOOKEAN) {
-    static_assert(R::SIMP, "neo-Hookean gather records: affine simplices");
-    constexpr int N = R::N;
-    double* out = rec + c * R::SIZE;
-    double Ji[GD][GD];
-    const double det = fabs(simplex_geometry<GD>(M, c, Ji));
-#pragma unroll
-    for (int i = 0; i < GD; ++i)
-#pragma unroll
-      for (int k = 0; k < GD; ++k) out[i * GD + k] = Ji[i][k];
-    out[N] = det;
-    if (R::QOFF > N + 1) out[N + 1] = 0.0;
-    double lam, mu;
-    cell_lame(F, c, lam, mu);
-    const int32_t* cn = M.cells + c * NN;
-    for (int q = 0; q < NQ; ++q) {
-      double Fq[N];
-      deformation_gradient<GD>(F.u, cn, NN, tab + NQ + q * NN * GD, Ji, Fq);
-      if constexpr (FA_NEO_INV) {
-        double I1 = GD == 2 ? 1.0 : 0.0, J;
-#pragma unroll
-        for (int m = 0; m < N; ++m) I1 = fma(Fq[m], Fq[m], I1);
-        if constexpr (GD == 2) J = Fq[0] * Fq[3] - Fq[1] * Fq[2];
-        else J = Fq[0] * (Fq[4] * Fq[8] - Fq[5] * Fq[7]) - Fq[1] * (Fq[3] * Fq[8] - Fq[5] * Fq[6]) +
-                 Fq[2] * (Fq[3] * Fq[7] - Fq[4] * Fq[6]);
-        double co[5];
-        neo_energy_coeffs(I1, J, lam, mu, co);
-        double* o = out + R::QOFF + q * R::QSTR;
-        if constexpr (FA_NEO_CREC) {
-          double Cm[GD][GD];
-          cofactor<GD>(Fq, Cm);
-#pragma unroll
-          for (int m = 0; m < N; ++m) o[m] = Cm[m / GD][m % GD];
-#pragma unroll
-          for (int t = 0; t < 3; ++t) o[N + t] = co[2 + t];
-#pragma unroll
-          for (int t = N + 3; t < R::QSTR; ++t) o[t] = 0.0;
-          continue;
-        }
-#pragma unroll
-        for (int m = 0; m < N; ++m) o[m] = Fq[m];
-#pragma unroll
-        for (int t = 0; t < 5; ++t) o[N + t] = co[t];
-#pragma unroll
-        for (int t = N + 5; t < R::QSTR; ++t) o[t] = 0.0;
-        continue;
-      }
-      using DD = Dual<Dual<double>>;
-      // the n(n+1)/2 hyper-dual passes unrolled: with compile-time one-hot seeds the compiler drops
-      // the zero derivative terms and evaluates the primal parts (F:F, det F, its log and inverse)
-      // once for all passes instead of once per pass
-#pragma unroll
-      for (int i = 0; i < N; ++i)
-#pragma unroll
-        for (int j = i; j < N; ++j) {
-          DD x[N];
-#pragma unroll
-          for (int m = 0; m < N; ++m) x[m] = DD{{Fq[m], m == i ? 1.0 : 0.0}, {m == j ? 1.0 : 0.0, 0.0}};
-          out[R::QOFF + q * R::QSTR + tri_index(i, j, N)] = neo_psi<GD, DD>(x, lam, mu).d.d;
-        }
-    }
-  } else {
+  {
   double r[R::SIZE];
   cell_record<GD, NN, NV, NQ, MAT>(M, F, tab, c, r);
   double2* out = reinterpret_cast<double2*>(rec + c * R::SIZE);
@@ -1444,7 +1294,7 @@ __global__ __launch_bounds__(256) void k_cell_records_staged(MeshView M, FormVie
                                                              const int8_t* __restrict__ bc, double* __restrict__ rec,
                                                              uint32_t* __restrict__ bcmask) {
   using R = Rec<GD, NV, NQ, MAT>;
-  static_assert(R::SIZE <= 16 && MAT != FA_NEO_HOOKEAN, "staged records: small records");
+  static_assert(R::SIZE <= 16, "staged records: small records");
   __shared__ __attribute__((aligned(16))) double sbuf[4][64 * R::SIZE];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double* sb = sbuf[wave];
@@ -1467,102 +1317,6 @@ __global__ __launch_bounds__(256) void k_cell_records_staged(MeshView M, FormVie
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (bcmask && valid) bcmask[c] = cell_bcmask<GD, NN>(M, bc, c);
-  }
-}
-
-// Neo-Hookean C records in 64-cell tiles (Rec::TILED): one wave per tile, lane = cell. Each block
-// of the tile (the 64 heads, then each quadrature point's 64 records) is written by the lanes into
-// a wave-private LDS buffer and stored as one contiguous run with 16 B per lane, instead of every
-// lane storing its own 464-B record (one cache line per lane per store instruction).
-template <int GD, int NN, int NV, int NQ>
-__global__ __launch_bounds__(256) void k_neo_records_tiled(MeshView M, FormView F, const double* __restrict__ tab,
-                                                           const int8_t* __restrict__ bc, double* __restrict__ rec,
-                                                           uint32_t* __restrict__ bcmask) {
-  using R = Rec<GD, NV, NQ, FA_NEO_HOOKEAN>;
-  static_assert(R::TILED && R::SIMP && NN * GD <= 32, "tiled neo-Hookean records");
-  constexpr int N = R::N, QO = R::QOFF, QS = R::QSTR;
-  constexpr int BUF = 64 * (QO > QS ? QO : QS);
-  __shared__ __attribute__((aligned(16))) double sbuf[4][BUF];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  double* sb = sbuf[wave];
-  auto wave_sync = [] {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
-  auto flush = [&](double* dst, int n) {  // sb[0, n) -> dst, n even, dst 16-B aligned
-    wave_sync();
-    const double2* s2 = reinterpret_cast<const double2*>(sb);
-    double2* d2 = reinterpret_cast<double2*>(dst);
-    for (int t = lane; t < n / 2; t += 64) d2[t] = s2[t];
-    wave_sync();
-  };
-  const int64_t ntiles = (M.ncells + 63) / 64;
-  for (int64_t tile = blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
-    const int64_t c0 = tile * 64 + lane;
-    const bool valid = c0 < M.ncells;
-    const int64_t c = valid ? c0 : M.ncells - 1;  // lanes past the end fill the tile's padding
-    double* tb = rec + tile * (64 * R::SIZE);
-    double Ji[GD][GD];
-    const double det = fabs(simplex_geometry<GD>(M, c, Ji));
-    double lam, mu;
-    cell_lame(F, c, lam, mu);
-    const double sgn = lam > 0.0 ? 1.0 : (lam < 0.0 ? -1.0 : 0.0);  // sign of W_JJ + W_J/J = lam / J^2
-#pragma unroll
-    for (int i = 0; i < GD; ++i)
-#pragma unroll
-      for (int k = 0; k < GD; ++k) sb[lane * QO + i * GD + k] = Ji[i][k];
-    sb[lane * QO + N] = det;
-#pragma unroll
-    for (int t = N + 1; t < QO; ++t) sb[lane * QO + t] = 0.0;
-    if constexpr (R::SREC) {
-      sb[lane * QO + N + 1] = sgn;
-      sb[lane * QO + N + 2] = mu;  // 2 W_1 of neo_energy (W is mu/2 I1 + terms in J)
-    }
-    flush(tb, 64 * QO);
-    const int32_t* cn = M.cells + c * NN;
-    for (int q = 0; q < NQ; ++q) {
-      double Fq[N];
-      deformation_gradient<GD>(F.u, cn, NN, tab + NQ + q * NN * GD, Ji, Fq);
-      double I1 = GD == 2 ? 1.0 : 0.0, J;
-#pragma unroll
-      for (int m = 0; m < N; ++m) I1 = fma(Fq[m], Fq[m], I1);
-      if constexpr (GD == 2) J = Fq[0] * Fq[3] - Fq[1] * Fq[2];
-      else J = Fq[0] * (Fq[4] * Fq[8] - Fq[5] * Fq[7]) - Fq[1] * (Fq[3] * Fq[8] - Fq[5] * Fq[6]) +
-               Fq[2] * (Fq[3] * Fq[7] - Fq[4] * Fq[6]);
-      double co[5];
-      neo_energy_coeffs(I1, J, lam, mu, co);
-      double Cm[GD][GD];
-      cofactor<GD>(Fq, Cm);
-      if constexpr (R::SREC) {
-        const double a2 = fabs(co[2]);
-        const double sc = sgn != 0.0 ? sqrt(a2) : 1.0;
-        const double rho = sgn != 0.0 ? co[3] / a2 : co[3];
-#pragma unroll
-        for (int m = 0; m < N; ++m) sb[lane * QS + m] = sc * Cm[m / GD][m % GD];
-        sb[lane * QS + N] = rho;
-#pragma unroll
-        for (int t = N + 1; t < QS; ++t) sb[lane * QS + t] = 0.0;
-      } else {
-#pragma unroll
-        for (int m = 0; m < N; ++m) sb[lane * QS + m] = Cm[m / GD][m % GD];
-#pragma unroll
-        for (int t = 0; t < 3; ++t) sb[lane * QS + N + t] = co[2 + t];
-#pragma unroll
-        for (int t = N + 3; t < QS; ++t) sb[lane * QS + t] = 0.0;
-      }
-      flush(tb + 64 * QO + q * (64 * QS), 64 * QS);
-    }
-    if (bcmask && valid) {
-      uint32_t m = 0;
-#pragma unroll
-      for (int b = 0; b < NN; ++b) {
-        const int64_t n = cn[b];
-#pragma unroll
-        for (int j = 0; j < GD; ++j) m |= (bc[n * GD + j] ? 1u : 0u) << (b * GD + j);
-      }
-      bcmask[c] = m;
-    }
   }
 }
 
@@ -1659,224 +1413,15 @@ __device__ __forceinline__ void lds_add_block(double* acc, int s, double (&K)[GD
     for (int jj = 0; jj < GD; ++jj) atomicAdd(&acc[s * (GD * GD) + i * GD + jj], K[i][jj]);
 }
 
-// ------------------------------------------------------------------------------------ barycentric blocks
-// Affine P1 / P2 simplex blocks without a reference-tensor table (FA_GATHER_BARY). With barycentric
-// coordinates lambda_0..lambda_d and their (scaled, physical) gradients g_k, every basis gradient is
-// grad phi_b = sum_l c_bl(lambda) g_l with c linear in lambda: vertex b = i: c_bi = 4 lambda_i - 1;
-// edge b = (i, j): c_bi = 4 lambda_j, c_bj = 4 lambda_i (P1: c_bb = 1). The exact integrals
-// int c_ak c_bl / |T| = B (1 + [x_ak = x_bl]) + C(type a, type b), x = the lambda in c, give
-//   G_ab = int grad phi_a grad phi_b^T = |T| [ (B + C) sigma_a sigma_b^T + B sum_x tau_a(x) tau_b(x)^T ]
-// with sigma_a = sum of a's gradients and tau_a(x) the gradient whose coefficient is in lambda_x.
-// B = 16 / ((d+1)(d+2)); C = 1 - 8/(d+1) (vertex-vertex), -4/(d+1) (vertex-edge), 0 (edge-edge).
-// The P2 integrand is quadratic, so this equals the default (exact) quadrature rule up to rounding.
-// The row node a is per item (selected from registers once), the item's columns are compile-time
-// (a static split of the cell's nodes), so a block is ~30 FP64 operations and no LDS table read.
-template <int GD, int NN>
-struct Bary {
-  static constexpr int NV = GD + 1;
-  static constexpr bool P2 = NN > NV;
-  static constexpr int NPART = (GD == 2 && !P2) ? 1 : 2;
-  static constexpr int NB = NN / NPART;
-  // static columns of each part: P2 tet {v0 v1 e(2,3) e(1,3) e(1,2)} {v2 v3 e(0,3) e(0,2) e(0,1)}
-  __host__ __device__ static constexpr int col(int part, int bb) {
-    if (GD == 3 && P2) return part == 0 ? (bb < 2 ? bb : 2 + bb) : (bb < 2 ? 2 + bb : 5 + bb);
-    if (GD == 2 && P2) return part == 0 ? (bb < 2 ? bb : 3) : (bb == 0 ? 2 : 3 + bb);
-    return part * NB + bb;  // P1: vertices in order
-  }
-  // barycentric pair (p, q) of local node b (p = q for a vertex); basix edge order
-  __host__ __device__ static constexpr int ep(int b) {
-    return b < NV ? b : (GD == 3 ? (int)((0x000112u >> (4 * (b - 4))) & 15u) : (int)((0x001u >> (4 * (b - 3))) & 15u));
-  }
-  __host__ __device__ static constexpr int eq(int b) {
-    return b < NV ? b : (GD == 3 ? (int)((0x123233u >> (4 * (b - 4))) & 15u) : (int)((0x122u >> (4 * (b - 3))) & 15u));
-  }
-  static constexpr double TREF = GD == 3 ? 1.0 / 6.0 : 0.5;
-  static constexpr double B = 16.0 / ((GD + 1) * (GD + 2)) * TREF;
-  static constexpr double KVV = (16.0 / ((GD + 1) * (GD + 2)) + 1.0 - 8.0 / (GD + 1)) * TREF;
-  static constexpr double KVE = (16.0 / ((GD + 1) * (GD + 2)) - 4.0 / (GD + 1)) * TREF;
-  static constexpr double KEE = B;
-};
-
-// The NB blocks of one item: row node `aloc` of a cell whose uniform-nu record holds s Ji (rows =
-// s grad lambda_1..d) and sign(mu |J|) in r[GD*GD]; `sl` = accumulator slots of the static columns.
-template <int GD, int NN, int PART>
-__device__ __forceinline__ void bary_blocks(const double* r, int aloc, const int* sl, uint32_t mask, double* acc,
-                                            double rlm, bool negw, int& bad, int maxb) {
-  using Bc = Bary<GD, NN>;
-  constexpr int NV = GD + 1, BS2 = GD * GD;
-  double g[NV][GD];
-#pragma unroll
-  for (int k = 1; k < NV; ++k)
-#pragma unroll
-    for (int d = 0; d < GD; ++d) g[k][d] = r[(k - 1) * GD + d];
-#pragma unroll
-  for (int d = 0; d < GD; ++d) {
-    double t = g[1][d];
-#pragma unroll
-    for (int k = 2; k < NV; ++k) t += g[k][d];
-    g[0][d] = -t;
-  }
-  // row side (dynamic a): its gradient(s), sigma_a and B tau_a(x)
-  const bool av = aloc < NV;
-  int ia = aloc, ja = -1;
-  if constexpr (Bc::P2) {
-    if (!av) { ia = Bc::ep(aloc); ja = Bc::eq(aloc); }
-  }
-  double gi[GD], gj[GD], sig[GD];
-#pragma unroll
-  for (int d = 0; d < GD; ++d) {
-    double vi = g[0][d], vj = g[0][d];
-#pragma unroll
-    for (int k = 1; k < NV; ++k) {
-      vi = ia == k ? g[k][d] : vi;
-      vj = ja == k ? g[k][d] : vj;
-    }
-    gi[d] = vi;
-    gj[d] = av ? 0.0 : vj;
-    sig[d] = gi[d] + gj[d];
-  }
-  const uint32_t rowm = (mask >> (aloc * GD)) & ((1u << GD) - 1);
-#pragma unroll
-  for (int bb = 0; bb < Bc::NB; ++bb) {
-    const int b = Bc::col(PART, bb);
-    const int p = Bc::ep(b), q = Bc::eq(b);
-    const bool bv = b < NV;
-    // G = up gp^T + uq gq^T (P1: up = TREF g_a, uq = 0; P2 vertex column: uq = 0)
-    double up[GD], uq[GD];
-    if constexpr (!Bc::P2) {
-#pragma unroll
-      for (int d = 0; d < GD; ++d) {
-        up[d] = Bc::TREF * gi[d];
-        uq[d] = 0.0;
-      }
-    } else {
-      // u_p = k sigma_a + B tau_a(q), u_q = k sigma_a + B tau_a(p); tau_a(x) = gi if x = ja,
-      // (vertex a: gi, edge a: gj) if x = ia, else 0
-      const double k = bv ? (av ? Bc::KVV : Bc::KVE) : (av ? Bc::KVE : Bc::KEE);
-#pragma unroll
-      for (int d = 0; d < GD; ++d) {
-        const double tq = (q == ia) ? (av ? gi[d] : gj[d]) : (q == ja ? gi[d] : 0.0);
-        up[d] = fma(k, sig[d], Bc::B * tq);
-        const double tp = (p == ia) ? (av ? gi[d] : gj[d]) : (p == ja ? gi[d] : 0.0);
-        uq[d] = bv ? 0.0 : fma(k, sig[d], Bc::B * tp);
-      }
-    }
-    // K = (lam/mu) G + G^T + tr(G) I (mu |J| is in the record's scale s^2), element by element
-    // straight into the accumulator: no G / K arrays live (register pressure)
-    double tr = 0.0;
-#pragma unroll
-    for (int d = 0; d < GD; ++d) tr = fma(up[d], g[p][d], bv ? tr : fma(uq[d], g[q][d], tr));
-    const double sg = negw ? r[BS2] : 1.0;
-    int s = sl[bb];
-    bad |= s < 0;
-    s = s < 0 ? maxb : s;
-    const uint32_t colm = (mask >> (b * GD)) & ((1u << GD) - 1);
-    const bool anybc = __any((rowm | colm) != 0u);
-#pragma unroll
-    for (int i = 0; i < GD; ++i)
-#pragma unroll
-      for (int l = 0; l < GD; ++l) {
-        const double gil = bv ? up[i] * g[p][l] : fma(up[i], g[p][l], uq[i] * g[q][l]);
-        const double gli = bv ? up[l] * g[p][i] : fma(up[l], g[p][i], uq[l] * g[q][i]);
-        double v = i == l ? fma(rlm + 1.0, gil, tr) : fma(rlm, gil, gli);
-        v *= sg;
-        if (anybc && (((rowm >> i) | (colm >> l)) & 1u)) v = 0.0;
-        atomicAdd(&acc[s * BS2 + i * GD + l], v);
-      }
-    __builtin_amdgcn_sched_barrier(0);  // one block at a time: keeps the live set small
-  }
-}
-
 // Items are (adjacency entry, column-node group). NSPLIT groups split the cell's NN column
 // nodes so that a chunk exposes enough independent items to all 256 lanes.
-#ifndef FA_GATHER_WAVES
-#define FA_GATHER_WAVES 4  // min waves per SIMD: 4 -> <= 128 VGPRs (16 waves / CU); measured best
-#endif
-#ifndef FA_GATHER_PERMUTE
-#define FA_GATHER_PERMUTE 1  // measured +16 % on config E at n = 120 (fewer same-slot LDS adds per instruction)
-#endif
-#ifndef FA_GATHER_STORE
-#define FA_GATHER_STORE 0  // chunk stores: 0 non-temporal, 1 plain, 2 sc1 (write-through)
-#endif
-template <typename T>
-__device__ __forceinline__ void out_store(const T& v, T* p) {
-  if constexpr (FA_GATHER_STORE == 0) {
-    __builtin_nontemporal_store(v, p);
-  } else if constexpr (FA_GATHER_STORE == 1) {
-    *p = v;
-  } else {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-#ifndef FA_ORDER_KICKS
-// perturbation rounds of the plan's bank-order search (FEMASM_ORDER_KICKS at run time). Config E:
-// 0 -> LDS passes 0.648 of unordered, gather 48.5 ms, plan 3 s; 16 -> 0.568, 48.0 ms, 21 s;
-// 64 -> 0.533, 47.6 ms, 79 s. Default 0: 16 rounds cost ~18 s of setup for ~0.5 ms per assembly,
-// which a Newton solve (7 assemblies, doc.tex:2051) never earns back
-#define FA_ORDER_KICKS 0
-#endif
-#ifndef FA_GATHER_BATCH
-#define FA_GATHER_BATCH 2  // chunks per chunk-counter atomic: measured 1 50.7, 2 48.2, 8 48.2 ms (E); C 1.95 / 1.95 / 2.02
-#endif
-#ifndef FA_GATHER_SU
-#define FA_GATHER_SU 4  // 16-B values per thread per store batch (LDS reads issued together)
-#endif
-#ifndef FA_GATHER_BARY
-// 1: uniform-nu P1/P2 simplices with a plain slot map use barycentric blocks with static columns
-// (no reference-tensor table; ~30 instead of ~57 FP64 ops per block). Measured slower on config E
-// (57.1 ms at 3 waves/SIMD, 82.5 ms at 4 with spills, vs 49.9 ms for the bank-ordered table path):
-// the items are bound by LDS-atomic bank conflicts, which static columns cannot order away.
-#define FA_GATHER_BARY 0
-#endif
-#ifndef FA_GATHER_FUSEZERO
-#define FA_GATHER_FUSEZERO 0  // 1: each thread zeroes the values it stores (one barrier less; measured 49.8 vs 48.4 ms)
-#endif
-#ifndef FA_GATHER_PRIO
-#define FA_GATHER_PRIO 0  // 1: raise the wave priority while a workgroup streams its chunk out
-#endif
-#ifndef FA_GATHER_APIPE
-#define FA_GATHER_APIPE 0  // measured slower: 5 VGPR spills, config E 50.6 -> 55.2 ms
-#endif
-#ifndef FA_GATHER_UNROLL_B
-#define FA_GATHER_UNROLL_B 1
-#endif
-// Timing-only ablations of the affine-simplex gather (wrong results; tools/ablate.sh):
-// 3 no LDS adds, 4 no reference-tensor LDS reads, 6 no item loop (chunk setup + store only),
-// 7 no per-item global loads,
-// 8 no chunk store, 9 no record loads (column ids and bc mask still loaded)
-#ifndef FA_ABL
-#define FA_ABL 0
-#endif
-// timing-only ablations of the neo-Hookean gather items: 1 no per-point record loads, 2 no LDS adds
-#ifndef FA_NEO_ABL
-#define FA_NEO_ABL 0
-#endif
-#ifndef FA_GATHER_TIMING
-#define FA_GATHER_TIMING 0  // 1: per-phase shader-clock totals of the gather (measurement build)
-#endif
-#ifndef FA_OWN_TIMING
-#define FA_OWN_TIMING 0  // 1: per-phase shader-clock totals of k_gather_own (measurement build)
-#endif
-#if FA_GATHER_TIMING || FA_OWN_TIMING
-__device__ unsigned long long g_gather_timing[10];
-#endif
-#if FA_GATHER_TIMING
-#define GT_MARK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#else
-#define GT_MARK(v)
-#endif
-#ifndef FA_GATHER_AHAT_GLOBAL
-#define FA_GATHER_AHAT_GLOBAL 0  // 1: reference tensor read through the vector L1 instead of LDS
-#endif
-#ifndef FA_GATHER_CN_ALWAYS
-#define FA_GATHER_CN_ALWAYS 0
-#endif
-#ifndef FA_GATHER_IPF
-#define FA_GATHER_IPF 0  // affine simplices: the next chunk's first item loaded during this chunk's tail
-#endif
-#ifndef FA_GATHER_PIPE_NEO
-#define FA_GATHER_PIPE_NEO 0
-#endif
+// min waves per SIMD of k_gather: 4 -> <= 128 VGPRs (16 waves / CU); measured best
+constexpr int kGatherWaves = 4;
+// chunks per chunk-counter atomic of k_gather's dynamic schedule: measured 1 50.7, 2 48.2, 8 48.2 ms
+// (E); C 1.95 / 1.95 / 2.02
+constexpr int kGatherBatch = 2;
+// 16-B values per thread per store batch of k_gather's chunk stream (LDS reads issued together)
+constexpr int kGatherStoreBatch = 4;
 // Item -> lane order of the gather: consecutive adjacency entries belong to the same row and add
 // into the same LDS slots, so entry jj of a chunk with na entries goes to position
 // (jj * stride) mod na, stride coprime to na; (x * stride) mod na in 32-bit with a float
@@ -1892,20 +1437,11 @@ __device__ __forceinline__ int gather_perm(int jj, int na, int st, float inv) {
   return j < 0 ? j + na : (j >= na ? j - na : j);
 }
 
-#ifndef FA_BARY_WAVES
-#define FA_BARY_WAVES FA_GATHER_WAVES
-#endif
-// neo-Hookean column items (5 columns of K and their gradients live)
-#ifndef FA_NEO_WAVES
-#define FA_NEO_WAVES 2  // 5 columns x (P, K) + a tangent sub-block live: 242 VGPRs, no spills in the item
-#endif
-template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT, int VAR = 0>
-__global__ __launch_bounds__(256, VAR == 1 ? FA_BARY_WAVES
-                                  : (MAT == FA_NEO_HOOKEAN ? FA_NEO_WAVES : FA_GATHER_WAVES))
-void k_gather(GatherArgs P) {
+template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT>
+__global__ __launch_bounds__(256, kGatherWaves) void k_gather(GatherArgs P) {
   using R = Rec<GD, NV, NQ, MAT>;
   constexpr int BS2 = GD * GD;
-  constexpr int MAXB = gather_maxb(MAT == FA_NEO_HOOKEAN, BS2);
+  constexpr int MAXB = gather_maxb(false, BS2);
   // ordered slots pack (b << 10) | chunk-relative position: positions must stay below 1024
   static_assert(MAXB < 1024, "FA_GATHER_LDS too large for the packed ordered-slot map");
   constexpr bool SIMP = R::SIMP;
@@ -1915,12 +1451,12 @@ void k_gather(GatherArgs P) {
   __shared__ int32_t rowoff[kGatherMaxRows + 1];
   __shared__ uint8_t s_rowbc[kGatherMaxRows];  // constrained-dof bits of each chunk row
   __shared__ uint8_t adjrow[kGatherMaxAdj];
-  constexpr bool NEO = (MAT == FA_NEO_HOOKEAN);
-  constexpr bool TAB = (MAT != MAT_BLOCKS) && (NEO || !SIMP);  // quadrature tables staged in LDS
+  static_assert(MAT != FA_NEO_HOOKEAN, "neo-Hookean forms: k_gather_neo");
+  constexpr bool TAB = (MAT != MAT_BLOCKS) && !SIMP;  // quadrature tables staged in LDS
   __shared__ double s_w[TAB ? NQ : 1];
   __shared__ double s_dphi[TAB ? NQ * NN * GD : 1];
   constexpr bool AFFT = MAT == MAT_AFFT;
-  __shared__ double s_ahat[SIMP && !AFFT && !FA_GATHER_AHAT_GLOBAL && VAR == 0 ? NN * NN * BS2 : 1];
+  __shared__ double s_ahat[SIMP && !AFFT ? NN * NN * BS2 : 1];
   constexpr int P1D = AFFT ? (NN == 8 || NN == 4 ? 2 : (NN == 27 || NN == 9 ? 3 : 4)) : 1;  // 1-D nodes
   __shared__ double s_t1d[AFFT ? 3 * P1D * P1D : 1];
   __shared__ int s_lat[AFFT ? NN : 1];
@@ -1956,7 +1492,7 @@ void k_gather(GatherArgs P) {
   auto take_batch = [&](int q, unsigned long long c) {
     if ((int64_t)c < per) {
       const int64_t base = q * per + (int64_t)c;
-      const int64_t end = min(q * per + min((int64_t)c + FA_GATHER_BATCH, per), P.nchunks);
+      const int64_t end = min(q * per + min((int64_t)c + kGatherBatch, per), P.nchunks);
       if (base < end) {
         s_bat[0] = base;
         s_bat[1] = end;
@@ -1975,7 +1511,7 @@ void k_gather(GatherArgs P) {
       if (t == 8) break;
       const int q = (int)((blockIdx.x + t) & 7);
       if ((qdone >> q) & 1u) continue;
-      take_batch(q, atomicAdd(P.ctr + q, (unsigned long long)FA_GATHER_BATCH));
+      take_batch(q, atomicAdd(P.ctr + q, (unsigned long long)kGatherBatch));
     }
     return P.nchunks;
   };
@@ -2000,15 +1536,11 @@ void k_gather(GatherArgs P) {
   if (idx0 >= P.nchunks) return;  // whole workgroup idle
 
   if constexpr (MAT == MAT_BLOCKS) {
-  } else if constexpr (NEO) {
-    for (int t = tid; t < NQ; t += 256) s_w[t] = P.tab[t];
-    for (int t = tid; t < NQ * NN * GD; t += 256) s_dphi[t] = P.tab[NQ + t];
   } else if constexpr (AFFT) {
     for (int t = tid; t < 3 * P1D * P1D; t += 256) s_t1d[t] = P.t1d[t];
     for (int t = tid; t < NN; t += 256) s_lat[t] = (int)P.lat[t];
-  } else if constexpr (SIMP && !FA_GATHER_AHAT_GLOBAL && VAR == 0) {
-    for (int t = tid; t < NN * NN * BS2; t += 256) s_ahat[t] = P.ahat[t];
   } else if constexpr (SIMP) {
+    for (int t = tid; t < NN * NN * BS2; t += 256) s_ahat[t] = P.ahat[t];
   } else {
     for (int t = tid; t < NQ; t += 256) s_w[t] = P.tab[t];
     for (int t = tid; t < NQ * NN * GD; t += 256) s_dphi[t] = P.tab[NQ + t];
@@ -2091,58 +1623,23 @@ void k_gather(GatherArgs P) {
     for (int t = tid; t < nv2; t += 256) lds_zero16(acc + 2 * t);
   };
 
-  // neo-Hookean items hold large per-q tangents: the prefetch registers would spill there
-  constexpr bool PIPE = !NEO || FA_GATHER_PIPE_NEO;
   // consecutive adjacency entries belong to the same row and add into the same LDS slots (the
   // diagonal block of a vertex row gets ~24 adds); a stride coprime to na spreads rows over
-  // lanes. The NSPLIT parts of one entry stay on neighbouring lanes (they read the same cell
-  // record). (jp * stride) mod na in 32-bit with a float quotient estimate (x < 2^24: off by <= 1).
-  // (neo-Hookean: measured 3 % faster without the permutation, n = 120)
-  constexpr bool PERM = FA_GATHER_PERMUTE && !NEO;
+  // lanes (measured +16 % on config E at n = 120). The NSPLIT parts of one entry stay on
+  // neighbouring lanes (they read the same cell record).
   // kernels that can run a positional plan (the ordered-slot affine-simplex elasticity path)
-  constexpr bool POSM = (MAT == 0 || MAT == MAT_LINU || (MAT == MAT_AFFT && NN * GD <= 32) || NEO) && SIMP &&
-                        NN % NSPLIT == 0;
-  // barycentric blocks (bary_blocks): static column parts, one part per half (NSPLIT = 2) of the
-  // workgroup so a wave's items share their code path; needs the plain (unordered) slot map
-  // (a separate instantiation, VAR = 1: sharing one kernel with the table path costs registers)
-  constexpr bool BARY = VAR == 1;
-  static_assert(!BARY || (MAT == MAT_LINU && SIMP && Bary<GD, NN>::NPART == NSPLIT && Bary<GD, NN>::NB == NBG),
-                "barycentric gather: uniform-nu affine P1/P2 simplices");
-  auto perm_stride = [&](int na_) { return PERM ? gather_perm_stride(na_) : 1; };
-  auto perm = [&](int jj, int na_, int st, float inv) {
-    if constexpr (!PERM) return jj;
-    return gather_perm(jj, na_, st, inv);
-  };
-  // Item prefetch (affine-simplex records): the first item of a thread in the NEXT chunk is
-  // loaded after this chunk's items, so its latency hides behind the store / stage / barriers
-  // instead of heading the next chunk's critical path. Its adjacency entry is loaded at the top
-  // of this chunk.
-  constexpr bool IPF = FA_GATHER_IPF && SIMP && !NEO && MAT != MAT_BLOCKS && FA_ABL == 0;
-  constexpr int RLP = IPF ? R::SIZE : 2;
-  double pr[RLP];
-  int32_t pcn[NBG];  // column node ids (in-kernel search) or slot offsets (slot map)
-  uint32_t pmask = 0u;
-  int32_t pflat_n = 0, pj_n = 0;
-  bool have_pf = false;
+  constexpr bool POSM = (MAT == 0 || MAT == MAT_LINU || (MAT == MAT_AFFT && NN * GD <= 32)) && SIMP && NN % NSPLIT == 0;
+  auto perm_stride = [&](int na_) { return gather_perm_stride(na_); };
+  auto perm = [&](int jj, int na_, int st, float inv) { return gather_perm(jj, na_, st, inv); };
   Desc cur = load_desc(idx0);
   fetch(cur);
   stage_meta(cur);
-  if constexpr (FA_GATHER_FUSEZERO) {  // the whole accumulator once; the chunk stores keep it clean
-    double2* acc2 = reinterpret_cast<double2*>(acc);
-    for (int t = tid; t < ((MAXB + 1) * BS2) / 2; t += 256) acc2[t] = make_double2(0.0, 0.0);
-    if ((((MAXB + 1) * BS2) & 1) && tid == 0) acc[(MAXB + 1) * BS2 - 1] = 0.0;
-  } else {
-    zero_acc(cur);
-  }
+  zero_acc(cur);
   int64_t nchunk = idx1;   // chunk k+1 (its descriptor is loaded, its metadata staged next)
   int64_t nnchunk = idx2;  // chunk k+2 (its descriptor is loaded during chunk k)
   Desc nxt = nchunk < P.nchunks ? load_desc(nchunk) : cur;
   __syncthreads();
   int kpar = 0;
-#if FA_GATHER_TIMING
-  unsigned long long gt[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long gt_top = __builtin_amdgcn_s_memtime();
-#endif
   for (;;) {
   // chunk k+3: lane 0 issues the counter atomic here and resolves it after the items, so the
   // wait for its return (a vmcnt wait) does not head the chunk
@@ -2153,18 +1650,10 @@ void k_gather(GatherArgs P) {
       const int q = (int)((blockIdx.x + t) & 7);
       if (!((qdone >> q) & 1u)) { gq = q; break; }
     }
-    if (gq >= 0) gcand = atomicAdd(P.ctr + gq, (unsigned long long)FA_GATHER_BATCH);
+    if (gq >= 0) gcand = atomicAdd(P.ctr + gq, (unsigned long long)kGatherBatch);
   }
 
-  if (PIPE && nchunk < P.nchunks) fetch(nxt);  // lands while this chunk is assembled
-  if (IPF && nchunk < P.nchunks) {
-    const int na_n = (int)(nxt.a1 - nxt.a0);
-    if (tid < na_n * NSPLIT) {
-      // positional plan: entries in the plan's order, item it -> position it / NSPLIT
-      pj_n = (POSM && P.eadj != nullptr) ? tid / NSPLIT : perm(tid / NSPLIT, na_n, perm_stride(na_n), 1.0f / (float)na_n);
-      pflat_n = adj_src[nxt.a0 + pj_n];
-    }
-  }
+  if (nchunk < P.nchunks) fetch(nxt);  // lands while this chunk is assembled
   Desc nn2;  // chunk k+2's descriptor: loaded after the items (scalar loads), used from the next chunk on
 
   const int64_t r0 = cur.r0;
@@ -2189,17 +1678,11 @@ void k_gather(GatherArgs P) {
       acc[s * BS2 + i * GD + i] = P.diag;
     }
   }
-#if FA_ABL == 3
-  double abl_sink = 0.0;
-#endif
 
   const int nitems = na * NSPLIT;
   const int stride = perm_stride(na);
   const float inv_n = 1.0f / (float)na;
-  // the item body; FROMPF: the thread's first item, whose loads were issued during the
-  // previous chunk (compile-time flag, so the prefetch registers die at its end)
-  auto item = [&](const int it0, auto FROMPF) {
-    GT_MARK(gt_i0);
+  auto item = [&](const int it0) {
     const int part = it0 % NSPLIT;
     // positional plan: entries are staged in the plan's order and slots are chunk-relative
     const bool posm = POSM && P.eadj != nullptr;
@@ -2210,29 +1693,13 @@ void k_gather(GatherArgs P) {
     const int lr = posm ? 0 : adjrow[j];
     const int lo = posm ? 0 : rowoff[lr], hi = posm ? 0 : rowoff[lr + 1];
     // one record + the column nodes + the bc mask: all independent loads, issued together
-    // registers: NEO keeps only Ji, wdet; tensor cells read their per-q records in the q loop
-    constexpr int RL = NEO ? (R::SREC ? R::QOFF : ((BS2 + 2) & ~1)) : (SIMP || MAT == FA_ASYM_DAMAGE ? R::SIZE : 2);
+    // registers: tensor cells read their per-q records in the q loop
+    constexpr int RL = SIMP || MAT == FA_ASYM_DAMAGE ? R::SIZE : 2;
     double r[RL];
-#if FA_ABL == 7 || FA_ABL == 9
-#pragma unroll
-    for (int k = 0; k < RL; ++k) r[k] = 0.5 + 0.01 * k + 1e-9 * (double)c;
-#endif
-#if FA_ABL == 7
-    int32_t cn[NBG];
-#pragma unroll
-    for (int bb = 0; bb < NBG; ++bb) cn[bb] = cols[lo + (int)((c + bb) & 7)];
-    const uint32_t mask = 0u;
-#else
     int32_t cn[NBG];
     uint32_t mask;
-    if constexpr (decltype(FROMPF)::value) {  // prefetched during the previous chunk
-#pragma unroll
-      for (int k = 0; k < RL; ++k) r[k] = pr[k < RLP ? k : 0];
-#pragma unroll
-      for (int bb = 0; bb < NBG; ++bb) cn[bb] = pcn[bb];
-      mask = pmask;
-    } else {
-    if constexpr (MAT != MAT_BLOCKS && FA_ABL != 9) {
+    {
+    if constexpr (MAT != MAT_BLOCKS) {
       const double2* rp = reinterpret_cast<const double2*>(P.rec + R::head(c));
 #pragma unroll
       for (int k = 0; k < RL / 2; ++k) {
@@ -2241,7 +1708,7 @@ void k_gather(GatherArgs P) {
         r[2 * k + 1] = v.y;
       }
     }
-    if (!P.slots || FA_GATHER_CN_ALWAYS) {  // column node ids: only the in-kernel slot search needs them
+    if (!P.slots) {  // column node ids: only the in-kernel slot search needs them
 #pragma unroll
       for (int bb = 0; bb < NBG; ++bb) {
         const int b = part * NBG + bb;
@@ -2250,7 +1717,6 @@ void k_gather(GatherArgs P) {
     }
     mask = P.bcmask ? P.bcmask[c] : 0u;
     }
-#endif
 
     if constexpr (MAT == MAT_BLOCKS) {
       const double* Eb = P.rec + ((int64_t)c * NN + aloc) * NN * BS2;  // bc already applied
@@ -2284,250 +1750,7 @@ void k_gather(GatherArgs P) {
         s = s < 0 ? MAXB : s;
         lds_add_block<2>(acc, s, K, (mask >> (aloc * 2)) & 3u, (mask >> (b * 2)) & 3u);
       }
-    } else if constexpr (NEO) {
-      // K_ab[i][k] = sum_q sum_{J,L} P[J][L] A_q[(iJ)(kL)] with P = (w_q |J| ga) (x) gb: the outer
-      // product first, then each 3x3 sub-block A_ik of the symmetric tangent is read once and serves
-      // K[i][k] and K[k][i] (K[k][i] = sum P[L][J] A_ik[J][L]). Only P, K and one sub-block are live,
-      // where contracting the row gradient first (C[i][k][L], 27 values) held C and all 45 tangent
-      // values at once and spilled (133 VGPRs at 4 waves / SIMD).
-      constexpr int N = R::N;
-      const double* Aq0 = P.rec + c * R::SIZE + R::QOFF;
-      const double wdet = r[BS2];
-      // the item's columns: in the plan's bank-balanced order with their chunk-relative slots
-      // (positional plan: (b << 10) | position), else the cell's nodes of this part in order
-      int ocol[NBG], opos[NBG];
-      const bool ordered = posm && P.slot_order == NSPLIT;
-#pragma unroll
-      for (int bb = 0; bb < NBG; ++bb) {
-        if (ordered) {
-          const int v = (int)P.slots[(a0 + j) * NN + part * NBG + bb];
-          ocol[bb] = v >> 10;
-          opos[bb] = v & 1023;
-        } else {
-          ocol[bb] = min(part * NBG + bb, NN - 1);  // past-the-end columns: computed, never added
-          opos[bb] = -1;
-        }
-      }
-      double K[NBG][GD][GD];
-#pragma unroll
-      for (int bb = 0; bb < NBG; ++bb)
-#pragma unroll
-        for (int i = 0; i < GD; ++i)
-#pragma unroll
-          for (int k = 0; k < GD; ++k) K[bb][i][k] = 0.0;
-      if constexpr (FA_NEO_INV) {
-        // invariant form (neo_energy_coeffs), 14 record values per point, the next point's values
-        // loaded while this one is contracted: per column K_ab += c2 Ca Cb^T - c3 Cb Ca^T +
-        // c4 (ga.gb) I [+ c0 Fa Fb^T + c1 (Fa Cb^T + Ca Fb^T)], Ca = cof(F) ga, Fa = F ga
-        const double* Q0 = P.rec + R::point0(c);
-        constexpr int NL = R::SREC ? N + 1 : (FA_NEO_CREC ? N + 3 : N + 5);
-        double Qn[NL];
-#if FA_NEO_ABL == 1
-#pragma unroll
-        for (int t = 0; t < NL; ++t) Qn[t] = 0.25 + 0.01 * t + 1e-12 * (double)c;
-#else
-#pragma unroll
-        for (int t = 0; t < NL; ++t) Qn[t] = Q0[t];
-#endif
-#pragma unroll 1
-        for (int q = 0; q < NQ; ++q) {
-          double Qc[NL];
-#pragma unroll
-          for (int t = 0; t < NL; ++t) Qc[t] = Qn[t];
-#if FA_NEO_ABL != 1
-          {
-            const double* Qx = Q0 + min(q + 1, NQ - 1) * R::PSTR;  // next point (the last one re-reads)
-#pragma unroll
-            for (int t = 0; t < NL; ++t) Qn[t] = Qx[t];
-          }
-#endif
-          double ga[GD];
-#pragma unroll
-          for (int d = 0; d < GD; ++d) {
-            double sgd = 0.0;
-#pragma unroll
-            for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + aloc) * GD + k] * r[k * GD + d];
-            ga[d] = s_w[q] * wdet * sgd;
-          }
-          double Cm[GD][GD];
-          if constexpr (FA_NEO_CREC) {  // the record holds C = cof F
-#pragma unroll
-            for (int m = 0; m < N; ++m) Cm[m / GD][m % GD] = Qc[m];
-          } else {
-            double Fq[N];
-#pragma unroll
-            for (int m = 0; m < N; ++m) Fq[m] = Qc[m];
-            cofactor<GD>(Fq, Cm);
-          }
-          constexpr int CO = FA_NEO_CREC ? N - 2 : N;  // index of c0 (c0, c1 absent from C records)
-          // SREC: C' = sqrt|c2| C in the record, c2 -> the head's sign, c3 -> rho, c4 -> the head's mu
-          const double c0 = FA_NEO_CREC ? 0.0 : Qc[min(CO, NL - 1)], c1 = FA_NEO_CREC ? 0.0 : Qc[min(CO + 1, NL - 1)],
-                       c2 = R::SREC ? r[N + 1] : Qc[min(CO + 2, NL - 1)], c3 = R::SREC ? Qc[N] : Qc[min(CO + 3, NL - 1)],
-                       c4 = R::SREC ? r[N + 2] : Qc[min(CO + 4, NL - 1)];
-          double u[GD], v[GD];
-#pragma unroll
-          for (int i = 0; i < GD; ++i) {
-            double ca = 0.0;
-#pragma unroll
-            for (int J = 0; J < GD; ++J) ca = fma(Cm[i][J], ga[J], ca);
-            u[i] = c2 * ca;
-            v[i] = c3 * ca;
-          }
-          // W_11 = W_1J = 0 for this energy: the F terms only where a lane has them (wave-uniform)
-          const bool mixed = !FA_NEO_CREC && __any(c0 != 0.0 || c1 != 0.0);
-          double w[GD];
-          if (mixed) {
-#pragma unroll
-            for (int i = 0; i < GD; ++i) {
-              double ca = 0.0, fa = 0.0;
-#pragma unroll
-              for (int J = 0; J < GD; ++J) {
-                ca = fma(Cm[i][J], ga[J], ca);
-                fa = fma(Qc[i * GD + J], ga[J], fa);
-              }
-              u[i] = fma(c1, fa, u[i]);
-              w[i] = c0 * fa + c1 * ca;
-            }
-          }
-#pragma unroll
-          for (int bb = 0; bb < NBG; ++bb) {
-            const int b = ocol[bb];
-            double gb[GD], Cb[GD], dot = 0.0;
-#pragma unroll
-            for (int d = 0; d < GD; ++d) {
-              double sgd = 0.0;
-#pragma unroll
-              for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + b) * GD + k] * r[k * GD + d];
-              gb[d] = sgd;
-              dot = fma(ga[d], sgd, dot);
-            }
-#pragma unroll
-            for (int k = 0; k < GD; ++k) {
-              double t = 0.0;
-#pragma unroll
-              for (int L = 0; L < GD; ++L) t = fma(Cm[k][L], gb[L], t);
-              Cb[k] = t;
-            }
-#pragma unroll
-            for (int i = 0; i < GD; ++i)
-#pragma unroll
-              for (int k = 0; k < GD; ++k) {
-                double t = fma(u[i], Cb[k], K[bb][i][k]);
-                t = fma(-Cb[i], v[k], t);
-                if (i == k) t = fma(c4, dot, t);
-                K[bb][i][k] = t;
-              }
-            if (mixed) {
-#pragma unroll
-              for (int k = 0; k < GD; ++k) {
-                double fb = 0.0;
-#pragma unroll
-                for (int L = 0; L < GD; ++L) fb = fma(Qc[k * GD + L], gb[L], fb);
-#pragma unroll
-                for (int i = 0; i < GD; ++i) K[bb][i][k] = fma(w[i], fb, K[bb][i][k]);
-              }
-            }
-          }
-        }
-      } else {
-#pragma unroll 1
-      for (int q = 0; q < NQ; ++q) {
-        double ga[GD];
-#pragma unroll
-        for (int d = 0; d < GD; ++d) {
-          double sgd = 0.0;
-#pragma unroll
-          for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + aloc) * GD + k] * r[k * GD + d];
-          ga[d] = s_w[q] * wdet * sgd;
-        }
-        double gb[NBG][GD];  // column gradients of the item
-#pragma unroll
-        for (int bb = 0; bb < NBG; ++bb) {
-          const int b = ocol[bb];
-#pragma unroll
-          for (int d = 0; d < GD; ++d) {
-            double sgd = 0.0;
-#pragma unroll
-            for (int k = 0; k < GD; ++k) sgd += s_dphi[(q * NN + b) * GD + k] * r[k * GD + d];
-            gb[bb][d] = sgd;
-          }
-        }
-        const double* Aq = Aq0 + q * R::QSTR;
-        // per 3x3 sub-block A_ik of the tangent (loaded once per item): the row gradient is
-        // contracted first, C[L] = sum_J ga[J] A_ik[J][L] (and C'[L] = sum_J ga[J] A_ik[L][J] for
-        // K[k][i]), then C is applied to every column: 81 + 27 NBG FMAs per point, and only ga, the
-        // columns' gb and K, one sub-block and C live
-#pragma unroll
-        for (int i = 0; i < GD; ++i) {
-#pragma unroll
-          for (int k = i; k < GD; ++k) {
-            double Ab[GD][GD];
-#pragma unroll
-            for (int J = 0; J < GD; ++J)
-#pragma unroll
-              for (int L = 0; L < GD; ++L)
-                Ab[J][L] = (i == k && L < J) ? 0.0 : Aq[tri_index(i * GD + J, k * GD + L, N)];
-            if (i == k) {
-#pragma unroll
-              for (int J = 0; J < GD; ++J)
-#pragma unroll
-                for (int L = 0; L < J; ++L) Ab[J][L] = Ab[L][J];  // symmetric diagonal sub-block
-            }
-            double C[GD], Ct[GD];
-#pragma unroll
-            for (int L = 0; L < GD; ++L) {
-              double t = 0.0, u = 0.0;
-#pragma unroll
-              for (int J = 0; J < GD; ++J) {
-                t = fma(ga[J], Ab[J][L], t);
-                if (i != k) u = fma(ga[J], Ab[L][J], u);
-              }
-              C[L] = t;
-              Ct[L] = u;
-            }
-#pragma unroll
-            for (int bb = 0; bb < NBG; ++bb) {
-              double t1 = K[bb][i][k];
-#pragma unroll
-              for (int L = 0; L < GD; ++L) t1 = fma(C[L], gb[bb][L], t1);
-              K[bb][i][k] = t1;
-              if (i != k) {
-                double t2 = K[bb][k][i];
-#pragma unroll
-                for (int L = 0; L < GD; ++L) t2 = fma(Ct[L], gb[bb][L], t2);
-                K[bb][k][i] = t2;
-              }
-            }
-          }
-        }
-      }
-      }
-#pragma unroll
-      for (int bb = 0; bb < NBG; ++bb) {
-        if (part * NBG + bb >= NN) break;
-        const int b = ocol[bb];
-        int s = ordered ? opos[bb]
-                        : (P.slots ? lo + (int)P.slots[(a0 + j) * NN + b] : lds_slot(cols, lo, hi, cn[bb], niter));
-        bad |= s < 0;
-        s = s < 0 ? MAXB : s;
-#if FA_NEO_ABL == 2
-        if (K[bb][0][0] == 1.2345e-300) acc[s * BS2] = K[bb][1][1];
-#else
-        lds_add_block<GD>(acc, s, K[bb], (mask >> (aloc * GD)) & ((1u << GD) - 1), (mask >> (b * GD)) & ((1u << GD) - 1));
-#endif
-      }
     } else if constexpr (SIMP) {
-      if constexpr (BARY) {
-        {
-          int slb[NBG];
-#pragma unroll
-          for (int bb = 0; bb < NBG; ++bb) slb[bb] = lo + (int)P.slots[(a0 + j) * NN + Bary<GD, NN>::col(part, bb)];
-          const bool negw_b = __any(r[BS2] < 0.0);  // wave-uniform: a cell with mu |J| < 0
-          if (part == 0) bary_blocks<GD, NN, 0>(r, aloc, slb, mask, acc, P.rlm, negw_b, bad, MAXB);
-          else bary_blocks<GD, NN, (Bary<GD, NN>::NPART > 1 ? 1 : 0)>(r, aloc, slb, mask, acc, P.rlm, negw_b, bad, MAXB);
-          return;
-        }
-      }
       // affine simplex: G_ab = |J| Ji^T Ahat_ab Ji  (reference-tensor form)
       constexpr bool LINU = MAT == MAT_LINU || MAT == MAT_AFFT;
       // LINU: r = s Ji, r[BS2] = sign; LIN: r = Ji, |J|, lam, mu
@@ -2540,19 +1763,7 @@ void k_gather(GatherArgs P) {
       uint64_t bcp = 0;
 #pragma unroll
       for (int bb = 0; bb < NBG; ++bb) bcp |= (uint64_t)(part * NBG + bb) << (6 * bb);
-      if (decltype(FROMPF)::value && P.slots) {  // prefetched slot map entries
-        if (P.slot_order) {  // (b << 10) | position
-#pragma unroll
-          for (int bb = 0; bb < NBG; ++bb) {
-            const int v = cn[bb];
-            sl[bb] = lo + (v & 1023);
-            bcp = (bcp & ~((uint64_t)63 << (6 * bb))) | ((uint64_t)(v >> 10) << (6 * bb));
-          }
-        } else {
-#pragma unroll
-          for (int bb = 0; bb < NBG; ++bb) sl[bb] = lo + cn[bb];
-        }
-      } else if (P.slots && P.slot_order) {  // (b << 10) | position, in bank-conflict-aware order
+      if (P.slots && P.slot_order) {  // (b << 10) | position, in bank-conflict-aware order
 #pragma unroll
         for (int bb = 0; bb < NBG; ++bb) {
           const int v = (int)P.slots[(a0 + j) * NN + part * NBG + bb];
@@ -2566,41 +1777,17 @@ void k_gather(GatherArgs P) {
       } else {
         lds_slots<NBG>(cols, lo, hi, cn, niter, sl);
       }
-#if FA_GATHER_TIMING
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      const unsigned long long gt_i1 = __builtin_amdgcn_s_memtime();
-      gt[7] += gt_i1 - gt_i0;
-#endif
       // constrained-dof bits: from the cell's mask, or -- cells with more dofs than mask bits -- from
       // the chunk row's bits and the column node's markers (only in waves holding such a cell)
       constexpr bool BIGM = NN * GD > 32;
       const uint32_t rowm = BIGM ? (mask ? (uint32_t)s_rowbc[lr] : 0u) : (mask >> (aloc * GD)) & ((1u << GD) - 1);
-      const double* Ah0 = (FA_GATHER_AHAT_GLOBAL ? P.ahat : s_ahat) + aloc * NN * BS2;
+      const double* Ah0 = s_ahat + aloc * NN * BS2;
       const int alat = AFFT ? s_lat[aloc] : 0;
-      // Reference-tensor reads one block ahead: block bb+1's table entry is read before block
-      // bb's adds are issued, so the wait for it (an in-order lgkmcnt) does not also wait for
-      // those nine LDS atomics to complete (FA_GATHER_APIPE=0: read at the top of each block)
-      constexpr bool APIPE = FA_GATHER_APIPE && NN % NSPLIT == 0 && FA_ABL != 4;
-      double Ahn[BS2];
-      int bnext = (int)(bcp & 63);
-      if constexpr (APIPE) {
-#pragma unroll
-        for (int e = 0; e < BS2; ++e) Ahn[e] = Ah0[bnext * BS2 + e];
-      }
-#pragma unroll FA_GATHER_UNROLL_B
+#pragma unroll 1
       for (int bb = 0; bb < NBG; ++bb) {
         if (NN % NSPLIT != 0 && part * NBG + bb >= NN) break;
-#if FA_ABL == 10
-        if (bb >= 1) break;  // timing only: one block per item
-#endif
-        const int b = APIPE ? bnext : (int)(bcp & 63);  // rolled loop: shift the column list like the slot list
+        const int b = (int)(bcp & 63);  // rolled loop: shift the column list like the slot list
         bcp >>= 6;
-#if FA_ABL == 4
-        double Ahr[BS2];
-#pragma unroll
-        for (int e = 0; e < BS2; ++e) Ahr[e] = 0.1 * (e + aloc) + bb;
-        const double* Ahp = Ahr;
-#else
         double Ahc[BS2];
         if constexpr (AFFT) {
           // reference tensor of an affine tensor cell from the 1-D matrices, then the uniform-nu
@@ -2632,10 +1819,9 @@ void k_gather(GatherArgs P) {
             for (int k = 0; k < GD; ++k) Ahc[i * GD + k] = fma(P.rlm, A[i][k], A[k][i]);
         } else {
 #pragma unroll
-          for (int e = 0; e < BS2; ++e) Ahc[e] = APIPE ? Ahn[e] : Ah0[b * BS2 + e];
+          for (int e = 0; e < BS2; ++e) Ahc[e] = Ah0[b * BS2 + e];
         }
         const double* Ahp = Ahc;
-#endif
         double T[GD][GD];  // T = Ahat Ji
 #pragma unroll
         for (int i = 0; i < GD; ++i)
@@ -2676,24 +1862,11 @@ void k_gather(GatherArgs P) {
         } else {
           lin_block<GD>(G, lam, mu, K);
         }
-        if constexpr (APIPE) {
-          if (bb + 1 < NBG) {
-            bnext = (int)(bcp & 63);
-#pragma unroll
-            for (int e = 0; e < BS2; ++e) Ahn[e] = Ah0[bnext * BS2 + e];
-          }
-        }
         int s = sl[0];  // rolled loop: shift the slot list instead of indexing it
 #pragma unroll
         for (int k = 0; k + 1 < NBG; ++k) sl[k] = sl[k + 1];
         bad |= s < 0;
         s = s < 0 ? MAXB : s;
-#if FA_ABL == 3
-#pragma unroll
-        for (int i = 0; i < GD; ++i)
-#pragma unroll
-          for (int jj = 0; jj < GD; ++jj) abl_sink += K[i][jj] * (double)s;
-#else
         uint32_t colm;
         if constexpr (BIGM) {
           colm = 0u;
@@ -2706,11 +1879,7 @@ void k_gather(GatherArgs P) {
           colm = (mask >> (b * GD)) & ((1u << GD) - 1);
         }
         lds_add_block<GD>(acc, s, K, rowm, colm);
-#endif
       }
-#if FA_GATHER_TIMING
-      gt[8] += __builtin_amdgcn_s_memtime() - gt_i1;
-#endif
     } else {
       // non-affine tensor cells: J^-1 per quadrature point, read from the record as the rolled
       // q loop needs it; only the per-column accumulators G stay live
@@ -2772,24 +1941,19 @@ void k_gather(GatherArgs P) {
   };
   {
     int it0 = tid;
-    if (IPF && have_pf) {
-      if (it0 < nitems) item(it0, std::true_type{});
-      it0 += 256;
-    }
-#if FA_ABL != 6
-    if constexpr (MAT == MAT_BLOCKS && FA_EB_WAVE) {
+    if constexpr (MAT == MAT_BLOCKS) {
       if (P.slots) {
         // element blocks: one wave per adjacency entry, its NN blocks (NN * 9 contiguous values of
         // Eb[c][a][.]) streamed with coalesced 8-B-per-lane loads, one LDS add per value (a lane's
         // block b = idx / 9 and entry e = idx % 9), instead of one lane reading NSPLIT whole blocks
         const int lane = tid & 63, wv = tid >> 6;
         constexpr int NEV = NN * BS2, NR = (NEV + 63) / 64;
-        // FA_EB_UNROLL entries per wave in flight (their loads issued together)
-        for (int j0 = wv * FA_EB_UNROLL; j0 < na; j0 += 4 * FA_EB_UNROLL) {
-          double v[FA_EB_UNROLL][NR];
-          int sl[FA_EB_UNROLL][NR], lo[FA_EB_UNROLL];
+        // kEbUnroll entries per wave in flight (their loads issued together)
+        for (int j0 = wv * kEbUnroll; j0 < na; j0 += 4 * kEbUnroll) {
+          double v[kEbUnroll][NR];
+          int sl[kEbUnroll][NR], lo[kEbUnroll];
 #pragma unroll
-          for (int w = 0; w < FA_EB_UNROLL; ++w) {
+          for (int w = 0; w < kEbUnroll; ++w) {
             const int j = min(j0 + w, na - 1);
             const int32_t pflat = s_adj[j];
             const int64_t c = pflat / NN;
@@ -2805,7 +1969,7 @@ void k_gather(GatherArgs P) {
             }
           }
 #pragma unroll
-          for (int w = 0; w < FA_EB_UNROLL; ++w) {
+          for (int w = 0; w < kEbUnroll; ++w) {
             if (j0 + w >= na) break;
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
@@ -2818,48 +1982,10 @@ void k_gather(GatherArgs P) {
           }
         }
       } else {
-        for (; it0 < nitems; it0 += 256) item(it0, std::false_type{});
+        for (; it0 < nitems; it0 += 256) item(it0);
       }
-    } else if constexpr (BARY) {
-      // part = tid / (256 / NSPLIT): whole waves per part; entry jj of the chunk on lane tid % (256 / NSPLIT)
-      constexpr int LPP = 256 / NSPLIT;
-      for (int jj = tid % LPP; jj < na; jj += LPP) item(jj * NSPLIT + tid / LPP, std::false_type{});
     } else {
-      for (; it0 < nitems; it0 += 256) item(it0, std::false_type{});
-    }
-#endif
-  }
-#if FA_ABL == 3
-  if (abl_sink == 1.2345) acc[0] = abl_sink;
-#endif
-  have_pf = false;
-  if (IPF && nchunk < P.nchunks) {
-    have_pf = true;
-    const int na_n = (int)(nxt.a1 - nxt.a0);
-    if (tid < na_n * NSPLIT) {
-      const int64_t c = pflat_n / NN;
-      const int part = tid % NSPLIT;
-      const double2* rp = reinterpret_cast<const double2*>(P.rec + c * R::SIZE);
-#pragma unroll
-      for (int k = 0; k < RLP / 2; ++k) {
-        double2 v = rp[k];
-        pr[2 * k] = v.x;
-        pr[2 * k + 1] = v.y;
-      }
-      if (P.slots) {
-#pragma unroll
-        for (int bb = 0; bb < NBG; ++bb) {
-          const int b = part * NBG + bb;
-          pcn[bb] = b < NN ? (int32_t)P.slots[((int64_t)nxt.a0 + pj_n) * NN + b] : 0;
-        }
-      } else {
-#pragma unroll
-        for (int bb = 0; bb < NBG; ++bb) {
-          const int b = part * NBG + bb;
-          pcn[bb] = b < NN ? P.M.cells[c * NN + b] : -1;
-        }
-      }
-      pmask = P.bcmask ? P.bcmask[c] : 0u;
+      for (; it0 < nitems; it0 += 256) item(it0);
     }
   }
   nn2 = nnchunk < P.nchunks ? load_desc(nnchunk) : nxt;
@@ -2872,9 +1998,7 @@ void k_gather(GatherArgs P) {
     s_idx[kpar] = ch;
   }
   if (bad) atomicOr(P.err, 1);
-  GT_MARK(gt_b);
   __syncthreads();
-  GT_MARK(gt_c);
   if (MAT == MAT_BLOCKS && P.bc) {
     for (int t = tid; t < nrows * GD; t += 256) {
       const int lr = t / GD, i = t % GD;
@@ -2885,14 +2009,7 @@ void k_gather(GatherArgs P) {
     }
     __syncthreads();
   }
-  if (nchunk < P.nchunks) {  // chunk k+1's metadata: every lane is past chunk k's items
-    if (!PIPE) fetch(nxt);
-    stage_meta(nxt);
-  }
-#if FA_GATHER_TIMING
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  gt[9] += __builtin_amdgcn_s_memtime() - gt_c;
-#endif
+  if (nchunk < P.nchunks) stage_meta(nxt);  // chunk k+1's metadata: every lane is past chunk k's items
   // Stream the chunk out: 16-B non-temporal stores (the matrix is written once and not re-read
   // by this launch, so it should not evict the records and dofmap the next chunks share).
   {
@@ -2900,28 +2017,13 @@ void k_gather(GatherArgs P) {
     double* out = P.A.data + off;
     const int nv = nb * BS2;
     const int h = (int)(off & 1);  // one leading double when the chunk starts on an odd double
-#if FA_ABL == 8
-    if (acc[tid] == 1.2345e-300) out[tid] = 0.0;  // timing only: no chunk store
-    if (false) {
-#endif
-#if FA_GATHER_PRIO
-    __builtin_amdgcn_s_setprio(3);
-#endif
-    // FA_GATHER_FUSEZERO: every accumulator value is read by exactly one thread here, which
-    // writes 0 back after reading it, so the accumulator is clean for the next chunk without a
-    // separate pass and its barrier (values past this chunk were never dirtied: zeroed once at
-    // the start, and items only add inside their chunk)
-    constexpr bool FZ = FA_GATHER_FUSEZERO;
-    if (h && tid == 0) {
-      out_store(acc[0], out);
-      if (FZ) acc[0] = 0.0;
-    }
+    if (h && tid == 0) __builtin_nontemporal_store(acc[0], out);
     const int np = (nv - h) >> 1;
     typedef double dv2 __attribute__((ext_vector_type(2)));
     dv2* out2 = reinterpret_cast<dv2*>(out + h);
     // a batch's LDS reads are issued together, then its stores (one LDS latency per batch,
     // not per store: the LDS is busy with other workgroups' atomics)
-    constexpr int SU = FA_GATHER_SU;
+    constexpr int SU = kGatherStoreBatch;
     for (int t0 = tid; t0 < np; t0 += 256 * SU) {
       dv2 v[SU];
 #pragma unroll
@@ -2932,46 +2034,17 @@ void k_gather(GatherArgs P) {
           else v[u] = reinterpret_cast<const dv2*>(acc)[t];
         }
       }
-      if (FZ) {
-#pragma unroll
-        for (int u = 0; u < SU; ++u) {
-          const int t = t0 + 256 * u;
-          if (t < np) {
-            if (h) { acc[1 + 2 * t] = 0.0; acc[2 + 2 * t] = 0.0; }
-            else reinterpret_cast<dv2*>(acc)[t] = dv2{0.0, 0.0};
-          }
-        }
-      }
 #pragma unroll
       for (int u = 0; u < SU; ++u) {
         const int t = t0 + 256 * u;
-        if (t < np) out_store(v[u], out2 + t);
+        if (t < np) __builtin_nontemporal_store(v[u], out2 + t);
       }
     }
-    if (((nv - h) & 1) && tid == 0) {
-      out_store(acc[nv - 1], out + nv - 1);
-      if (FZ) acc[nv - 1] = 0.0;
-    }
-#if FA_GATHER_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
-#if FA_ABL == 8
-    }
-#endif
+    if (((nv - h) & 1) && tid == 0) __builtin_nontemporal_store(acc[nv - 1], out + nv - 1);
   }
-  GT_MARK(gt_d);
-#if FA_GATHER_TIMING
-  gt[0] += gt_b - gt_top;
-  gt[1] += gt_c - gt_b;
-  gt[2] += gt_d - gt_c;
-  gt[6] += 1;
-#endif
   if (nchunk >= P.nchunks) break;
-  if constexpr (!FA_GATHER_FUSEZERO) {
-    __syncthreads();  // the store has read acc
-    zero_acc(nxt);
-  }
-  GT_MARK(gt_e);
+  __syncthreads();  // the store has read acc
+  zero_acc(nxt);
   cur = nxt;
   nxt = nn2;
   nchunk = nnchunk;
@@ -2979,19 +2052,8 @@ void k_gather(GatherArgs P) {
                   : chunk_of(vb + 3 * vstep);
   kpar ^= 1;
   vb += vstep;
-  GT_MARK(gt_f);
   __syncthreads();
-#if FA_GATHER_TIMING
-  gt_top = __builtin_amdgcn_s_memtime();
-  gt[3] += gt_e - gt_d;
-  gt[4] += gt_f - gt_e;
-  gt[5] += gt_top - gt_f;
-#endif
   }
-#if FA_GATHER_TIMING
-  if ((tid & 63) == 0)
-    for (int k = 0; k < 10; ++k) atomicAdd(&g_gather_timing[k], gt[k]);
-#endif
 }
 
 // ------------------------------------------------------------------------------ store-decoupled gather
@@ -3013,25 +2075,15 @@ void k_gather(GatherArgs P) {
 // be a conditional vector-memory operation), XCD-contiguous. Dirichlet diagonals are set after the
 // launch (k_bc_diag), items zero every constrained entry as in k_gather. Plans: <= 256 items per
 // chunk (fa_plan_gather caps a chunk at 256 / NSPLIT adjacency entries for these elements).
-#ifndef FA_LIN_NT
-#define FA_LIN_NT 1  // k_gather_lin chunk stores: 1 non-temporal, 0 plain
-#endif
+// chunk stores: non-temporal (plain stores measured 53.5 vs 49.8 ms on config E)
 template <typename T>
 __device__ __forceinline__ void lin_store(const T& v, T* p) {
-  if constexpr (FA_LIN_NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
+  __builtin_nontemporal_store(v, p);
 }
 
-// chunk drain without the read / zero barrier (chunk_drain): 1, or the two-barrier read-all /
-// zero-all drain: 0. k_gather_lin keeps the two-barrier drain: at its 128-VGPR cap chunk_drain's
-// buffer descriptor and pair registers spill uniform pointers whose reloads wait vmcnt(0) in the
-// item loop, i.e. for every chunk store in flight
-#ifndef FA_DRAIN_LIN
-#define FA_DRAIN_LIN 0
-#endif
-#ifndef FA_DRAIN_NEO
-#define FA_DRAIN_NEO 1
-#endif
+// chunk drain of k_gather_neo without the read / zero barrier (chunk_drain); k_gather_lin keeps the
+// two-barrier read-all / zero-all drain (at its 128-VGPR cap chunk_drain's buffer descriptor and pair
+// registers spill uniform pointers whose reloads wait vmcnt(0) in the item loop)
 // Stream a chunk's nv accumulated values acc[h, h + nv) to out[0, nv) and leave the accumulator
 // zero, after the items barrier. The values form 16-B pairs acc2[j], j < j1 = (h + nv + 1) / 2; pair
 // j lands at out - h + 2j, 16-B aligned (out - h is). A lane reads, zeroes and stores its own pairs
@@ -3053,7 +2105,7 @@ __device__ __forceinline__ void chunk_drain(double* acc, int h, int nv, double* 
   // dropped by the range check (no traffic), so every lane issues the same stores
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out - h, 0, (h + nv) * 8, 0x00020000);
   constexpr int OOB = 0x40000000;
-  constexpr int AUX = FA_LIN_NT ? 2 : 0;  // nt
+  constexpr int AUX = 2;  // nt
   double hv = 0.0, tv = 0.0;
 #pragma unroll
   for (int u = 0; u < SW; ++u) {
@@ -3070,19 +2122,11 @@ __device__ __forceinline__ void chunk_drain(double* acc, int h, int nv, double* 
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rs,
                                         (tid == (jt % NT) && tail_half && !(jt == 0 && h)) ? 8 * (h + nv - 1) : OOB, 0, AUX);
 }
-#ifndef FA_LIN_FUSE
-#define FA_LIN_FUSE 1  // P1 simplices (fa_assemble_matrix): records formed inside k_gather_lin
-#endif
-#ifndef FA_LIN_P1GRAD
-#define FA_LIN_P1GRAD 1  // P1 simplices: blocks from the gradients in the record, no table (k_gather_lin)
-#endif
-#ifndef FA_LIN_ABL
-// timing-only ablations of k_gather_lin (wrong results; tools/lin_ablate.sh): 1 plain read-add-write
-// instead of LDS atomics (races), 2 no accumulator adds, 3 no table reads, 4 no chunk stores,
-// 5 no item loads (constant records / slots)
-#define FA_LIN_ABL 0
-#endif
-template <int GD, int NN, int NSPLIT, int NT = 256, bool FUSE = false>
+constexpr int FA_LIN_FUSE = 1;  // P1 simplices (fa_assemble_matrix): records formed inside k_gather_lin
+// 2^e for a normal exponent (|e| <= 1022), from its bits (no FP64 op: uniform e stays scalar)
+__device__ __forceinline__ double pow2(int e) { return __hiloint2double((e + 1023) << 20, 0); }
+
+template <int GD, int NN, int NSPLIT, int NT = 256, bool FUSE = false, bool FIX = false>
 __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32_t* __restrict__ zero32,
                                                         double* __restrict__ dump, int64_t per) {
   using R = Rec<GD, GD + 1, 1, MAT_LINU>;
@@ -3094,10 +2138,11 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
   constexpr int SW = (MAXB * BS2 / 2 + NT - 1) / NT;  // pair stores per lane per chunk
   constexpr int RL = R::SIZE;
   static_assert(NN % NSPLIT == 0 && NN * GD <= 32 && RL % 2 == 0 && NN <= 63, "k_gather_lin: affine simplices");
-  constexpr bool P1G = NN == GD + 1 && FA_LIN_P1GRAD;
+  constexpr bool P1G = NN == GD + 1;
   typedef double dv2 __attribute__((ext_vector_type(2)));
   __shared__ __attribute__((aligned(16))) double acc[2 * NP2];
   __shared__ double tab[NN * NN * BS2];
+  __shared__ uint32_t s_fx[2];  // FIX: scale exponent of the chunks of each parity (max over their items)
   dv2* acc2 = reinterpret_cast<dv2*>(acc);
   const int tid = threadIdx.x;
   // Chunk schedule: rounds of G consecutive chunks; in each round the 8 XCDs take 8 adjacent blocks
@@ -3113,6 +2158,7 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
   (void)per;
   for (int t = tid; t < NN * NN * BS2; t += NT) tab[t] = P.ahat[t];
   for (int t = tid; t < NP2; t += NT) acc2[t] = dv2{0.0, 0.0};
+  if (tid < 2) s_fx[tid] = 0u;
 
   const int64_t abase = sload(P.A.indptr, P.A.row_begin);
   const int64_t nent = P.M.ncells * NN;
@@ -3156,15 +2202,6 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
   };
   auto load_item = [&](const Desc& d, int32_t pflat, Item& it, const Vid& vd) {
     const int64_t c = pflat / NN;
-#if FA_LIN_ABL == 5
-#pragma unroll
-    for (int k = 0; k < RL; ++k) it.r[k] = 0.5 + 0.01 * k + 1e-9 * (double)c;
-    const int na5 = (int)(d.a1 - d.a0);
-#pragma unroll
-    for (int bb = 0; bb < NBG; ++bb) it.sl[bb] = ((uint32_t)((part * NBG + bb) % NN) << 10) | (uint32_t)((jit * 7 + bb * 13) % max(na5, 1));
-    it.mask = 0u;
-    return;
-#endif
     if constexpr (FUSE) {
       uint32_t m = 0u;
 #pragma unroll
@@ -3212,6 +2249,33 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
       it.r[GD * GD] = s2 < 0.0 ? -1.0 : 1.0;
     }
   };
+  // FIX (deterministic mode): every contribution v of chunk k is added as the integer
+  // round(v * 2^se_k) with ds_add_u64, so a block's sum is exact and independent of the order of
+  // the adds; the drain converts it back (one rounding). se_k = 1072 - e_k with e_k the largest
+  // biased exponent of the chunk's item bounds fixc * rho^2 >= |block entry|, so |v * 2^se| < 2^50
+  // (the 1.5 * 2^52 rounding constant below is exact there) and up to 2^13 contributions never
+  // overflow. The chunk's e_k is the max over its items (per wave by DPP, then one ds_max_u32 per
+  // wave into s_fx[k & 1]), formed at the end of chunk k-1 from its prefetched items.
+  auto bound_exp = [&](const Item& it, bool v) -> uint32_t {
+    double rho = 0.0;
+#pragma unroll
+    for (int kk = 0; kk < BS2; ++kk) rho += fabs(it.r[kk]);
+    const double m = P.fixc * rho * rho;
+    return v ? (uint32_t)((uint64_t)__double_as_longlong(m) >> 52) & 0x7FFu : 0u;
+  };
+  auto wave_max = [&](uint32_t e) -> uint32_t {
+    e = max(e, (uint32_t)__builtin_amdgcn_mov_dpp((int)e, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    e = max(e, (uint32_t)__builtin_amdgcn_mov_dpp((int)e, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    e = max(e, (uint32_t)__builtin_amdgcn_mov_dpp((int)e, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    e = max(e, (uint32_t)__builtin_amdgcn_mov_dpp((int)e, 0x140, 0xF, 0xF, false));  // row_mirror
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)e, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)e, 16);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)e, 32), dd = (uint32_t)__builtin_amdgcn_readlane((int)e, 48);
+    return max(max(a, b), max(c, dd));
+  };
+  auto post_bound = [&](const Item& it, const Desc& d, int slot) {
+    const uint32_t e = wave_max(bound_exp(it, jit < (int)(d.a1 - d.a0)));
+    if ((tid & 63) == 0) atomicMax(&s_fx[slot], e);
+  };
 
   Desc d0 = desc(0), d1 = desc(1), d2 = desc(2), d3 = desc(3);
   int32_t pf0 = load_entry(d0), pf1 = load_entry(d1), pf2 = FUSE ? load_entry(d2) : 0;
@@ -3229,6 +2293,11 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
   // loop's waits are not widened by pending prologue loads merged in at the loop head)
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();  // table and accumulator staged
+  if constexpr (FIX) {  // chunk 0's scale
+    form_record(cur);
+    post_bound(cur, d0, 0);
+    __syncthreads();
+  }
   for (int64_t k = 0; k < cnt; ++k) {
     // L1: chunk k+2's entry ids; L2: chunk k+1's records / slots / masks (before chunk k's stores)
     // (FUSE: entries of chunk k+3, vertex ids of chunk k+2, coordinates of chunk k+1)
@@ -3242,7 +2311,13 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
       load_item(d1, pf1, nxt, vid1);
     }
     const Desc d4 = desc(k + (FUSE ? 4 : 3));
-    form_record(cur);
+    if constexpr (!FIX) form_record(cur);  // FIX: formed at the end of the previous chunk (its bound)
+    int se = 0;
+    double S = 1.0;
+    if constexpr (FIX) {  // uniform: the scale's bits are built in SGPRs (2^se = (se + 1023) << 52)
+      se = __builtin_amdgcn_readfirstlane(max(-1000, min(1000, 1072 - (int)s_fx[k & 1])));
+      S = pow2(se);
+    }
     // items of chunk k
     const int64_t off = (d0.b0 - abase) * BS2;
     const int h = (int)(off & 1);
@@ -3306,13 +2381,8 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
         for (int e = 0; e < BS2; ++e) B[e] = Bn[e];
         if (bb + 1 < NBG) {  // next block's table entry: issued before this block's atomics
           const int b1 = (int)(cur.sl[bb + 1 < NBG ? bb + 1 : bb] >> 10);
-#if FA_LIN_ABL == 3
-#pragma unroll
-          for (int e = 0; e < BS2; ++e) Bn[e] = 0.1 * e + b1;
-#else
 #pragma unroll
           for (int e = 0; e < BS2; ++e) Bn[e] = Ah0[b1 * BS2 + e];
-#endif
         }
         // G = (s Ji)^T B (s Ji), column by column; K = G + tr(G) / (1 + r) I
 #pragma unroll
@@ -3358,35 +2428,28 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
         bad |= valid && s >= nb;
         if (valid && s < nb) {
           double* ap = acc + h + s * BS2;
-#if FA_LIN_ABL == 1
-          double o[BS2];
+          if constexpr (FIX) {
 #pragma unroll
-          for (int e = 0; e < BS2; ++e) o[e] = ap[e];
+            for (int i = 0; i < GD; ++i)
 #pragma unroll
-          for (int i = 0; i < GD; ++i)
+              for (int kk = 0; kk < GD; ++kk) {
+                // round(v * 2^se): v * 2^se + 1.5 * 2^52 has a unit ulp for |v * 2^se| < 2^51, and its
+                // bits minus those of 1.5 * 2^52 are that integer (two's complement)
+                const double t = fma(G[i][kk], S, 0x1.8p52);
+                const unsigned long long q = (unsigned long long)__double_as_longlong(t) - 0x4338000000000000ull;
+                atomicAdd(reinterpret_cast<unsigned long long*>(ap + i * GD + kk), q);
+              }
+          } else {
 #pragma unroll
-            for (int kk = 0; kk < GD; ++kk) ap[i * GD + kk] = o[i * GD + kk] + G[i][kk];
-#elif FA_LIN_ABL == 2
-          if (G[0][0] == 1.2345e-300) ap[0] = G[1][1];
-#elif FA_LIN_ABL == 6
+            for (int i = 0; i < GD; ++i)
 #pragma unroll
-          for (int i = 0; i < GD; ++i)
-#pragma unroll
-            for (int kk = 0; kk < GD; ++kk)
-              atomicAdd(reinterpret_cast<unsigned long long*>(ap + i * GD + kk), __builtin_bit_cast(unsigned long long, G[i][kk]));
-#else
-#pragma unroll
-          for (int i = 0; i < GD; ++i)
-#pragma unroll
-            for (int kk = 0; kk < GD; ++kk) atomicAdd(ap + i * GD + kk, G[i][kk]);
-#endif
+              for (int kk = 0; kk < GD; ++kk) atomicAdd(ap + i * GD + kk, G[i][kk]);
+          }
         }
       }
     }
     __syncthreads();  // B1: the chunk is accumulated
-    if constexpr (FA_DRAIN_LIN && FA_LIN_ABL != 4) {
-      chunk_drain<SW, NT>(acc, h, nb * BS2, P.A.data + off, dump, tid);
-    } else {
+    if (FIX && tid == 0) s_fx[k & 1] = 0u;  // read by every item above; next written for chunk k + 2
     // read the chunk into registers: pairs t (value 2t + h .. 2t + 1 + h at acc2[t + h]); lanes past
     // the chunk's pairs repeat the last pair, and every lane reads the unpaired head / tail value
     const int nv = nb * BS2;
@@ -3394,13 +2457,22 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     dv2 v[SW];
 #pragma unroll
     for (int u = 0; u < SW; ++u) v[u] = acc2[h + max(min(tid + NT * u, np - 1), 0)];
-    const double hv = acc[h], tv = acc[max(nv - 1, 0) + h];
+    double hv = acc[h], tv = acc[max(nv - 1, 0) + h];
+    if constexpr (FIX) {  // the integer sums back to doubles: (hi 2^32 + lo) 2^-se, one rounding
+      const double c32 = pow2(32 - se), inv = pow2(-se);
+      auto tod = [&](double x) -> double {
+        const long long q = __double_as_longlong(x);
+        return fma((double)(int)(q >> 32), c32, (double)(unsigned)q * inv);
+      };
+#pragma unroll
+      for (int u = 0; u < SW; ++u) v[u] = dv2{tod(v[u].x), tod(v[u].y)};
+      hv = tod(hv);
+      tv = tod(tv);
+    }
     __syncthreads();  // B2: every read is done before any zero
-#if FA_LIN_ABL != 7
 #pragma unroll
     for (int u = 0; u < SW; ++u)
       if (tid + NT * u < np) acc2[h + tid + NT * u] = dv2{0.0, 0.0};
-#endif
     // the unpaired head (acc[1] when h = 1) and tail sit in pairs whose other half is never written
     if (tid == 0) acc2[0] = dv2{0.0, 0.0};
     if (tid == 1) acc2[(max(nv - 1, 0) + h) >> 1] = dv2{0.0, 0.0};
@@ -3410,14 +2482,13 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     const bool none = np < 1;
     double* out = none ? dump : P.A.data + off;
     dv2* out2 = reinterpret_cast<dv2*>(none ? dump : out + h);
-#if FA_LIN_ABL == 4
-    if (hv == 1.2345e-300) out[0] = tv + v[0].x + v[SW - 1].y;
-#else
 #pragma unroll
     for (int u = 0; u < SW; ++u) lin_store(v[u], out2 + max(min(tid + NT * u, np - 1), 0));
     lin_store(hv, out);
     lin_store(tv, out + max(nv - 1, 0));
-#endif
+    if constexpr (FIX) {  // chunk k+1's scale from its prefetched items (records formed here for FUSE)
+      form_record(nxt);
+      post_bound(nxt, d1, (int)((k + 1) & 1));
     }
     __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics
     // rotate the pipeline
@@ -3592,54 +2663,21 @@ __global__ __launch_bounds__(256) void k_neo_records_m(MeshView M, FormView F, c
   }
 }
 
-#ifndef FA_NEOM_WAVES
-#define FA_NEOM_WAVES 2
-#endif
-// timing-only ablations of k_gather_neo (wrong results): 2 no accumulator adds, 4 no chunk stores
-#ifndef FA_NEOM_ABL
-#define FA_NEOM_ABL 0
-#endif
-#ifndef FA_NEOM_UONLY
-#define FA_NEOM_UONLY 0
-#endif
-#ifndef FA_NEOM_ROLL
-#define FA_NEOM_ROLL 0  // with FA_NEOM_QS=2 (and FA_NEOM_UONLY=1): the spill-free q-split build
-#endif
-#if FA_NEOM_ROLL
-#define FA_NEOM_ROLL_UNROLL 1
-#else
-#define FA_NEOM_ROLL_UNROLL 16
-#endif
-// Q-split items (QS = 2, P2 tetrahedra): each (entry, column part) item runs on a lane pair, one
-// lane per half of the quadrature points (half the record and the per-point W, Z in registers:
-// 4 instead of 2 waves / SIMD); the pair sums its partial blocks by DPP and each lane adds half of
-// the 9 entries into LDS. 512-thread workgroups keep 256 items (the neo plan's 128 entries) per chunk.
-#ifndef FA_NEOM_QS
-#define FA_NEOM_QS 1  // 2: q-split lane pairs, measured slower (E-neo 94 vs 77 ms: DPP sums and a rolled column loop, VALU +84 %)
-#endif
-template <int NQ>
-__host__ __device__ constexpr int neo_qsplit() { return NQ % FA_NEOM_QS == 0 ? FA_NEOM_QS : 1; }
-// the lane pair's sum of a double (quad_perm [1, 0, 3, 2]: swap with the neighbouring lane)
-__device__ __forceinline__ double pair_sum(double v) {
-  const int lo = __double2loint(v), hi = __double2hiint(v);
-  const int plo = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false);
-  const int phi = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false);
-  return v + __hiloint2double(phi, plo);
-}
-template <int GD, int NN, int NQ, int NSPLIT, int QS = 1>
-__global__ __launch_bounds__(256 * QS, QS == 2 ? 4 : FA_NEOM_WAVES) void k_gather_neo(GatherArgs P,
-                                                                                  const uint32_t* __restrict__ zero32,
-                                                                                  double* __restrict__ dump) {
+// 2 waves / SIMD (215 VGPRs, no spills in the item loop; 3 waves measured slower: spilled records)
+template <int GD, int NN, int NQ, int NSPLIT>
+__global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint32_t* __restrict__ zero32,
+                                                       double* __restrict__ dump) {
   using R = NeoM<GD, NQ>;
-  constexpr int NTH = 256 * QS;  // threads: 256 items
-  constexpr int BS2 = GD * GD, NT = R::NT, NQL = NQ / QS;
+  constexpr int NTH = 256;  // threads: 256 items
+  constexpr int BS2 = GD * GD, NT = R::NT, NQL = NQ;
   constexpr int NBG = NN / NSPLIT;
   constexpr int MAXB = gather_maxb(true, BS2);
   constexpr int NACC = MAXB * BS2 + 2;
   constexpr int NP2 = (NACC + 1) / 2;
-  constexpr int SW = (MAXB * BS2 / 2 + NTH - 1) / NTH;
-  constexpr int NE = (BS2 + QS - 1) / QS;  // block entries each lane of an item adds
-  static_assert(NN % NSPLIT == 0 && NN * GD <= 32 && NN <= 63 && MAXB < 1024 && NQ % QS == 0 && QS <= 2,
+  // pairs per lane of chunk_drain: a chunk spans up to (h + MAXB * BS2 + 1) / 2 16-B pairs
+  constexpr int SW = (MAXB * BS2 / 2 + 1 + NTH - 1) / NTH;
+  static_assert(SW * NTH >= (MAXB * BS2 + 1) / 2 + 1, "chunk_drain covers every pair");
+  static_assert(NN % NSPLIT == 0 && NN * GD <= 32 && NN <= 63 && MAXB < 1024,
                 "k_gather_neo: affine simplices");
   typedef double dv2 __attribute__((ext_vector_type(2)));
   __shared__ __attribute__((aligned(16))) double acc[2 * NP2];
@@ -3689,7 +2727,7 @@ __global__ __launch_bounds__(256 * QS, QS == 2 ? 4 : FA_NEOM_WAVES) void k_gathe
     const int64_t r0 = sload(P.row_start, c), r1 = sload(P.row_start, c + 1);
     return Desc{sload(P.A.indptr, r0), sload(P.A.indptr, r1), sload(P.adj_ptr, r0), sload(P.adj_ptr, r1)};
   };
-  const int item = tid / QS, qh = tid % QS;  // qh: this lane's half of the points
+  const int item = tid;
   const int jit = item / NSPLIT, part = item % NSPLIT;
   auto entry_of = [&](const Desc& d) -> int64_t {
     const int na = (int)(d.a1 - d.a0);
@@ -3713,7 +2751,7 @@ __global__ __launch_bounds__(256 * QS, QS == 2 ? 4 : FA_NEOM_WAVES) void k_gathe
     if constexpr (HL % 2) it.hd[HL - 1] = hq[HL - 1];
 #pragma unroll
     for (int ql = 0; ql < NQL; ++ql) {
-      const dv2* pp = reinterpret_cast<const dv2*>(P.rec + R::point(c, qh * NQL + ql));
+      const dv2* pp = reinterpret_cast<const dv2*>(P.rec + R::point(c, ql));
 #pragma unroll
       for (int k = 0; k < R::PT / 2; ++k) {
         const dv2 v = pp[k];
@@ -3746,12 +2784,11 @@ __global__ __launch_bounds__(256 * QS, QS == 2 ? 4 : FA_NEOM_WAVES) void k_gathe
       const int aloc = pf0 % NN;
       const uint32_t rowm = (cur.mask >> (aloc * GD)) & ((1u << GD) - 1);
       const double sc = cur.hd[NT];
-      // per point: U = M_q dphi_a, W = s_c U, Z = rho_q U (FA_NEOM_UONLY: U only, s_c V and rho_q V
-      // formed per block: 6 more multiplies per point and block, 12 fewer live doubles)
+      // per point: U = M_q dphi_a, W = s_c U, Z = rho_q U
       double W[NQL][GD], Z[NQL][GD];
 #pragma unroll
       for (int ql = 0; ql < NQL; ++ql) {
-        const int q = qh * NQL + ql;
+        const int q = ql;
         double pa[GD];
 #pragma unroll
         for (int kk = 0; kk < GD; ++kk) pa[kk] = s_phi[(aloc * NQ + q) * GD + kk];
@@ -3760,37 +2797,17 @@ __global__ __launch_bounds__(256 * QS, QS == 2 ? 4 : FA_NEOM_WAVES) void k_gathe
           double u = cur.pt[ql][i * GD] * pa[0];
 #pragma unroll
           for (int kk = 1; kk < GD; ++kk) u = fma(cur.pt[ql][i * GD + kk], pa[kk], u);
-          W[ql][i] = FA_NEOM_UONLY ? u : sc * u;
-          Z[ql][i] = FA_NEOM_UONLY ? 0.0 : cur.pt[ql][BS2] * u;
+          W[ql][i] = sc * u;
+          Z[ql][i] = cur.pt[ql][BS2] * u;
         }
       }
       lds_vdouble* Ta = (lds_vdouble*)(s_T + aloc * NN * NT);
-      const double dsel = qh == 0 ? 1.0 : 0.0;  // the mu term once per item
-      // rolled loop: the mu-term dots of the item's columns up front (S dies here), rotated per block
-      double dt[NBG];
-      if constexpr (FA_NEOM_ROLL) {
 #pragma unroll
-        for (int bb = 0; bb < NBG; ++bb) {
-          const int b = (int)((cur.sl[bb / 2] >> (16 * (bb % 2) + 10)) & 63u);
-          double dd = 0.0;
-#pragma unroll
-          for (int t = 0; t < NT; ++t) dd = fma(cur.hd[t], Ta[b * NT + t], dd);
-          dt[bb] = dsel * dd;
-        }
-      }
-      // QS = 2: the column loop rolled (FA_NEOM_ROLL): one block's values live at a time
-#pragma unroll FA_NEOM_ROLL_UNROLL
       for (int bb = 0; bb < NBG; ++bb) {
-        uint32_t slv;
-        if constexpr (FA_NEOM_ROLL) {
-          const uint64_t w01 = (uint64_t)cur.sl[0] | ((uint64_t)cur.sl[NSL > 1 ? 1 : 0] << 32);
-          slv = bb < 4 ? (uint32_t)(w01 >> (16 * bb)) & 0xFFFFu : (cur.sl[NSL - 1] >> 16 * (bb & 1)) & 0xFFFFu;
-        } else {
-          slv = (cur.sl[bb / 2] >> (16 * (bb % 2))) & 0xFFFFu;
-        }
+        const uint32_t slv = (cur.sl[bb / 2] >> (16 * (bb % 2))) & 0xFFFFu;
         const int s = (int)(slv & 1023u);
         const int b = (int)(slv >> 10);
-        lds_vdouble* pb = (lds_vdouble*)(s_phi + (b * NQ + qh * NQL) * GD);
+        lds_vdouble* pb = (lds_vdouble*)(s_phi + b * NQ * GD);
         double K[GD][GD];
 #pragma unroll
         for (int i = 0; i < GD; ++i)
@@ -3808,41 +2825,17 @@ __global__ __launch_bounds__(256 * QS, QS == 2 ? 4 : FA_NEOM_WAVES) void k_gathe
             for (int kk = 1; kk < GD; ++kk) v = fma(cur.pt[ql][i * GD + kk], pbq[kk], v);
             V[i] = v;
           }
-          if constexpr (FA_NEOM_UONLY) {
-            double sV[GD], rV[GD];
 #pragma unroll
-            for (int i = 0; i < GD; ++i) {
-              sV[i] = sc * V[i];
-              rV[i] = cur.pt[ql][BS2] * V[i];
-            }
+          for (int i = 0; i < GD; ++i)
 #pragma unroll
-            for (int i = 0; i < GD; ++i)
-#pragma unroll
-              for (int kk = 0; kk < GD; ++kk) K[i][kk] = fma(W[ql][i], sV[kk], fma(-rV[i], W[ql][kk], K[i][kk]));
-          } else {
-#pragma unroll
-            for (int i = 0; i < GD; ++i)
-#pragma unroll
-              for (int kk = 0; kk < GD; ++kk) K[i][kk] = fma(W[ql][i], V[kk], fma(-V[i], Z[ql][kk], K[i][kk]));
-          }
+            for (int kk = 0; kk < GD; ++kk) K[i][kk] = fma(W[ql][i], V[kk], fma(-V[i], Z[ql][kk], K[i][kk]));
         }
-        if constexpr (FA_NEOM_ROLL) {
-#pragma unroll
-          for (int i = 0; i < GD; ++i) K[i][i] += dt[0];
-#pragma unroll
-          for (int t = 0; t + 1 < NBG; ++t) dt[t] = dt[t + 1];
-        } else {
+        {
           double dot = 0.0;
 #pragma unroll
           for (int t = 0; t < NT; ++t) dot = fma(cur.hd[t], Ta[b * NT + t], dot);
 #pragma unroll
-          for (int i = 0; i < GD; ++i) K[i][i] = fma(dsel, dot, K[i][i]);
-        }
-        if constexpr (QS == 2) {
-#pragma unroll
-          for (int i = 0; i < GD; ++i)
-#pragma unroll
-            for (int kk = 0; kk < GD; ++kk) K[i][kk] = pair_sum(K[i][kk]);
+          for (int i = 0; i < GD; ++i) K[i][i] += dot;
         }
         const uint32_t colm = (cur.mask >> (b * GD)) & ((1u << GD) - 1);
         if (__any((rowm | colm) != 0u)) {
@@ -3855,24 +2848,10 @@ __global__ __launch_bounds__(256 * QS, QS == 2 ? 4 : FA_NEOM_WAVES) void k_gathe
         bad |= valid && s >= nb;
         if (valid && s < nb) {
           double* ap = acc + h + s * BS2;
-#if FA_NEOM_ABL == 2
-          if (K[0][0] == 1.2345e-300) ap[0] = K[1][1];
-#else
-          if constexpr (QS == 1) {
 #pragma unroll
-            for (int i = 0; i < GD; ++i)
+          for (int i = 0; i < GD; ++i)
 #pragma unroll
-              for (int kk = 0; kk < GD; ++kk) atomicAdd(ap + i * GD + kk, K[i][kk]);
-          } else {  // lane qh adds entries qh * NE .. qh * NE + NE - 1
-            const double* Kf = &K[0][0];
-#pragma unroll
-            for (int e = 0; e < NE; ++e) {
-              const int e1 = NE + e;
-              const double val = qh ? (e1 < BS2 ? Kf[e1 < BS2 ? e1 : 0] : 0.0) : Kf[e];
-              if (qh == 0 || e1 < BS2) atomicAdd(ap + qh * NE + e, val);
-            }
-          }
-#endif
+            for (int kk = 0; kk < GD; ++kk) atomicAdd(ap + i * GD + kk, K[i][kk]);
         }
       }
     }
@@ -3880,33 +2859,7 @@ __global__ __launch_bounds__(256 * QS, QS == 2 ? 4 : FA_NEOM_WAVES) void k_gathe
     // issued before chunk k's stores (their wait at chunk k+1 does not include the stores)
     load_item(d1, pf1, cur);
     __syncthreads();  // B1: the chunk is accumulated
-    if constexpr (FA_DRAIN_NEO && FA_NEOM_ABL != 4) {
-      chunk_drain<SW, NTH>(acc, h, nb * BS2, P.A.data + off, dump, tid);
-    } else {
-    const int nv = nb * BS2;
-    const int np = (nv - h) >> 1;
-    dv2 v[SW];
-#pragma unroll
-    for (int u = 0; u < SW; ++u) v[u] = acc2[h + max(min(tid + NTH * u, np - 1), 0)];
-    const double hv = acc[h], tv = acc[max(nv - 1, 0) + h];
-    __syncthreads();  // B2: every read is done before any zero
-#pragma unroll
-    for (int u = 0; u < SW; ++u)
-      if (tid + NTH * u < np) acc2[h + tid + NTH * u] = dv2{0.0, 0.0};
-    if (tid == 0) acc2[0] = dv2{0.0, 0.0};
-    if (tid == 1) acc2[(max(nv - 1, 0) + h) >> 1] = dv2{0.0, 0.0};
-    const bool none = np < 1;
-    double* out = none ? dump : P.A.data + off;
-    dv2* out2 = reinterpret_cast<dv2*>(none ? dump : out + h);
-#if FA_NEOM_ABL == 4
-    if (hv == 1.2345e-300) out[0] = tv + v[0].x + v[SW - 1].y;
-#else
-#pragma unroll
-    for (int u = 0; u < SW; ++u) lin_store(v[u], out2 + max(min(tid + NTH * u, np - 1), 0));
-    lin_store(hv, out);
-    lin_store(tv, out + max(nv - 1, 0));
-#endif
-    }
+    chunk_drain<SW, NTH>(acc, h, nb * BS2, P.A.data + off, dump, tid);
     __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics
     d0 = d1;
     d1 = d2;
@@ -3927,28 +2880,16 @@ __global__ __launch_bounds__(256 * QS, QS == 2 ? 4 : FA_NEOM_WAVES) void k_gathe
 // lanes, once per chunk). The chunk's distinct cells' records are staged in LDS once per chunk
 // (one 80-B load per cell instead of one per item), the reference-tensor table B_ab sits in LDS.
 // Output: the chunk is streamed to HBM with coalesced 16-B stores, exactly as k_gather does.
-#ifndef FA_OWN_LDS
-#define FA_OWN_LDS 28672  // output staging bytes per workgroup
-#endif
-#ifndef FA_OWN_CCAP
-#define FA_OWN_CCAP 256  // distinct cells (and adjacency entries) per chunk of a contribution plan (8-bit slots);
+constexpr int FA_OWN_LDS = 28672;  // output staging bytes per workgroup
+constexpr int FA_OWN_CCAP = 256;  // distinct cells (and adjacency entries) per chunk of a contribution plan (8-bit slots);
                          // config C 2.87 ms at 128 -> 2.07 at 256, A 0.155 -> 0.136 ms
-#endif
-#ifndef FA_OWN_WAVES
-#define FA_OWN_WAVES 3
-#endif
-// timing-only ablations of k_gather_own (wrong results): 1 no block writes (flush), 2 no table
-// reads, 3 no record reads, 4 no contribution loop (staging + store skeleton)
-#ifndef FA_OWN_ABL
-#define FA_OWN_ABL 0
-#endif
 __host__ __device__ constexpr int own_maxb(int bs2) { return FA_OWN_LDS / (8 * bs2) < 1023 ? FA_OWN_LDS / (8 * bs2) : 1023; }
 // contribution word (u16): bits 0-7 cell slot, 8-14 a * NN + b (127: padding), 15 last of its block
 constexpr uint32_t kOwnPad = 0x7F00u;
 constexpr uint32_t kOwnIdle = 0xFFFFu;  // lane start of a lane with no contribution
 
 template <int GD, int NN>
-__global__ __launch_bounds__(256, FA_OWN_WAVES) void k_gather_own(GatherArgs P) {
+__global__ __launch_bounds__(256, 3) void k_gather_own(GatherArgs P) {
   using R = Rec<GD, GD + 1, 1, MAT_LINU>;
   constexpr int BS2 = GD * GD, MAXB = own_maxb(BS2), NAB = NN * NN, RS = R::SIZE, CCAP = FA_OWN_CCAP;
   constexpr int KMAX = (CCAP * NN + 255) / 256;
@@ -4015,10 +2956,6 @@ __global__ __launch_bounds__(256, FA_OWN_WAVES) void k_gather_own(GatherArgs P) 
   pcell2 = (tid < CCAP && c1 < P.nchunks) ? P.ccells[c1 * CCAP + tid] : -1;
   stage();
   __syncthreads();
-#if FA_OWN_TIMING
-  unsigned long long ot[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long o0 = __builtin_amdgcn_s_memtime();
-#endif
   for (;;) {
     const int64_t c2 = chunk_of(v + 2 * gridDim.x);
     const int K = nwords(c);
@@ -4059,7 +2996,7 @@ __global__ __launch_bounds__(256, FA_OWN_WAVES) void k_gather_own(GatherArgs P) 
         }
       }
     };
-    if (start != kOwnIdle && FA_OWN_ABL != 4) {
+    if (start != kOwnIdle) {
 #pragma unroll
       for (int k = 0; k < KMAX; ++k) {
         if (k < K) {  // wave-uniform
@@ -4069,11 +3006,7 @@ __global__ __launch_bounds__(256, FA_OWN_WAVES) void k_gather_own(GatherArgs P) 
           const int ab = valid ? ab0 : 0;
           const int cs = valid ? (int)(w & 255u) : 0;
           double r[RS];
-          if (FA_OWN_ABL == 3) {
-#pragma unroll
-            for (int q = 0; q < RS; ++q) r[q] = 0.5 + 0.01 * q + 1e-3 * cs;
-            r[BS2] = 1.0;
-          } else {
+          {
             const double2* rp = reinterpret_cast<const double2*>(s_rec + cs * RS);
 #pragma unroll
             for (int q = 0; q < RS / 2; ++q) {
@@ -4082,14 +3015,7 @@ __global__ __launch_bounds__(256, FA_OWN_WAVES) void k_gather_own(GatherArgs P) 
               r[2 * q + 1] = t.y;
             }
           }
-#if FA_OWN_ABL == 2
-          double Ahr[BS2];
-#pragma unroll
-          for (int e = 0; e < BS2; ++e) Ahr[e] = 0.1 * e + 0.01 * ab;
-          const double* Ah = Ahr;
-#else
           const double* Ah = s_tab + ab * BS2;
-#endif
           double T[GD][GD];  // T = B_ab (s Ji)
 #pragma unroll
           for (int i = 0; i < GD; ++i)
@@ -4124,7 +3050,7 @@ __global__ __launch_bounds__(256, FA_OWN_WAVES) void k_gather_own(GatherArgs P) 
               double* o = s_out + pos * BS2;
 #pragma unroll
               for (int e = 0; e < BS2; ++e) {
-                if (FA_OWN_ABL != 1 || acc[e] == 1.2345e-300) o[e] = acc[e];
+                o[e] = acc[e];
                 acc[e] = 0.0;
               }
               ++pos;
@@ -4135,39 +3061,25 @@ __global__ __launch_bounds__(256, FA_OWN_WAVES) void k_gather_own(GatherArgs P) 
       }
     }
     if (open) finish(false);
-#if FA_OWN_TIMING
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const unsigned long long o1 = __builtin_amdgcn_s_memtime();
-#endif
     __syncthreads();  // every block's plain write is done; s_rec / s_wd / s_mask are free
-#if FA_OWN_TIMING
-    const unsigned long long o2 = __builtin_amdgcn_s_memtime();
-#endif
     if (open) {       // the segment ended inside a block: add the partial sum
       double* o = s_out + pos * BS2;
 #pragma unroll
       for (int e = 0; e < BS2; ++e) atomicAdd(o + e, acc[e]);
     }
     if (c1 < P.nchunks) stage();
-#if FA_OWN_TIMING
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    const unsigned long long o3 = __builtin_amdgcn_s_memtime();
-#endif
     __syncthreads();
-#if FA_OWN_TIMING
-    const unsigned long long o4 = __builtin_amdgcn_s_memtime();
-#endif
     {
       const int64_t b0 = sload(P.chunk_b, c), b1 = sload(P.chunk_b, c + 1);
       const int64_t off = (b0 - abase) * BS2;
       double* out = P.A.data + off;
       const int nv = (int)(b1 - b0) * BS2;
       const int h = (int)(off & 1);
-      if (h && tid == 0) out_store(s_out[0], out);
+      if (h && tid == 0) __builtin_nontemporal_store(s_out[0], out);
       const int np = (nv - h) >> 1;
       typedef double dv2 __attribute__((ext_vector_type(2)));
       dv2* out2 = reinterpret_cast<dv2*>(out + h);
-      constexpr int SU = FA_GATHER_SU;
+      constexpr int SU = kGatherStoreBatch;
       for (int t0 = tid; t0 < np; t0 += 256 * SU) {
         dv2 vv[SU];
 #pragma unroll
@@ -4181,34 +3093,17 @@ __global__ __launch_bounds__(256, FA_OWN_WAVES) void k_gather_own(GatherArgs P) 
 #pragma unroll
         for (int u = 0; u < SU; ++u) {
           const int t = t0 + 256 * u;
-          if (t < np) out_store(vv[u], out2 + t);
+          if (t < np) __builtin_nontemporal_store(vv[u], out2 + t);
         }
       }
-      if (((nv - h) & 1) && tid == 0) out_store(s_out[nv - 1], out + nv - 1);
+      if (((nv - h) & 1) && tid == 0) __builtin_nontemporal_store(s_out[nv - 1], out + nv - 1);
     }
-#if FA_OWN_TIMING
-    const unsigned long long o5 = __builtin_amdgcn_s_memtime();
-    ot[0] += o1 - o0;  // prefetch issue + contribution loop
-    ot[1] += o2 - o1;  // barrier after the loop
-    ot[2] += o3 - o2;  // partial atomics + staging (waits for the prefetched loads)
-    ot[3] += o4 - o3;  // barrier before the store
-    ot[4] += o5 - o4;  // store issue
-    ot[6] += 1;
-#endif
     if (c1 >= P.nchunks) break;
     __syncthreads();  // the store has read s_out
-#if FA_OWN_TIMING
-    o0 = __builtin_amdgcn_s_memtime();
-    ot[5] += o0 - o5;  // barrier after the store
-#endif
     c = c1;
     c1 = c2;
     v += gridDim.x;
   }
-#if FA_OWN_TIMING
-  if ((tid & 63) == 0)
-    for (int k = 0; k < 8; ++k) atomicAdd(&g_gather_timing[k], ot[k]);
-#endif
 }
 
 // ------------------------------------------------------------------------------------ adjacency
@@ -4459,15 +3354,14 @@ extern "C" int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const
 // slots is chosen to minimise sum over steps of the largest residue count (the passes), with the
 // sum of squared counts as tie-break: identity start, then pairwise step swaps per lane until no
 // swap improves. The slot map then holds (b << 10) | position in that order. One thread per
-// (chunk, quarter). stats (optional): {passes, identity passes, lower bound} summed.
+// (chunk, quarter).
 // Positional plans (eperm != NULL): position jj of a chunk holds entry eperm[a0 + jj]; the plain
 // map is read from src and written by position, with chunk-relative block positions.
 template <int NN, int NSPLIT>
 __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64_t* __restrict__ indptr,
                               const int64_t* __restrict__ adj_ptr, int64_t nchunks, int groups_per_chunk,
                               uint16_t* __restrict__ slots, const uint16_t* __restrict__ src,
-                              const uint16_t* __restrict__ eperm, unsigned long long* __restrict__ stats, int kicks,
-                              int stats_rot) {
+                              const uint16_t* __restrict__ eperm) {
   constexpr int NBG = NN / NSPLIT, Q = 16;
   const int64_t total = nchunks * groups_per_chunk;
   for (int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gid < total;
@@ -4485,7 +3379,6 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
     const float inv = 1.0f / (float)na;
     const int nl = min(Q, nitems - p0);
     uint16_t off[Q][NBG];
-    uint16_t posv[Q][NBG];  // chunk-relative block position (stats only)
     uint8_t res[Q][NBG], pick[Q][NBG];
     uint8_t cnt[NBG][16];
     int64_t ent[Q];
@@ -4493,8 +3386,6 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
     const uint16_t* rd = eperm ? src : slots;
     for (int t = 0; t < NBG; ++t)
       for (int r = 0; r < 16; ++r) cnt[t][r] = 0;
-    int deg[16];
-    for (int r = 0; r < 16; ++r) deg[r] = 0;
     for (int q = 0; q < nl; ++q) {
       const int p = p0 + q;
       const int part = p % NSPLIT;
@@ -4511,22 +3402,11 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
       ent[q] = (eperm ? a0 + p / NSPLIT : e) * NN + part * NBG;
       for (int t = 0; t < NBG; ++t) {
         off[q][t] = rd[ein + t];
-        posv[q][t] = (uint16_t)(rowlo + off[q][t]);
         res[q][t] = (uint8_t)((rowlo + off[q][t]) & 15);
         pick[q][t] = (uint8_t)t;
         ++cnt[t][res[q][t]];
-        ++deg[res[q][t]];
       }
     }
-    auto step_max = [&](int t) {
-      int m = 0;
-      for (int r = 0; r < 16; ++r) m = max(m, (int)cnt[t][r]);
-      return m;
-    };
-    int ident = 0, lb = NBG, dmax = 0;
-    for (int t = 0; t < NBG; ++t) ident += step_max(t);
-    for (int r = 0; r < 16; ++r) dmax = max(dmax, deg[r]);
-    lb = max(lb, dmax);
     // step maxima and how many residues reach them: a swap is then priced in O(1) and the two
     // steps are recounted only when it is taken
     int mx[NBG], nmx[NBG];
@@ -4575,71 +3455,7 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
         if (!improved) break;
       }
     };
-    auto total = [&]() {
-      int c = 0;
-      for (int t = 0; t < NBG; ++t) c += mx[t];
-      return c;
-    };
     descend();
-    // iterated local search: random pairs of swaps, descend again, keep the best order
-    int best = total();
-    uint8_t bestp[Q][NBG];
-    for (int q = 0; q < nl; ++q)
-      for (int t = 0; t < NBG; ++t) bestp[q][t] = pick[q][t];
-    uint32_t rng = 2654435761u * (uint32_t)(gid + 1);
-    for (int k = 0; k < kicks && best > lb; ++k) {
-      for (int j = 0; j < 2; ++j) {
-        rng ^= rng << 13; rng ^= rng >> 17; rng ^= rng << 5;
-        const int q = (int)(rng % (uint32_t)nl), t1 = (int)((rng >> 8) % NBG), t2 = (int)((rng >> 16) % NBG);
-        if (t1 != t2) swap_pick(q, t1, t2);
-      }
-      descend();
-      const int c = total();
-      if (c <= best) {
-        best = c;
-        for (int q = 0; q < nl; ++q)
-          for (int t = 0; t < NBG; ++t) bestp[q][t] = pick[q][t];
-      } else {  // back to the best order
-        for (int t = 0; t < NBG; ++t)
-          for (int r = 0; r < 16; ++r) cnt[t][r] = 0;
-        for (int q = 0; q < nl; ++q)
-          for (int t = 0; t < NBG; ++t) {
-            pick[q][t] = bestp[q][t];
-            ++cnt[t][res[q][pick[q][t]]];
-          }
-        for (int t = 0; t < NBG; ++t) recount(t);
-      }
-    }
-    if (stats) {
-      int cost = 0;
-      for (int t = 0; t < NBG; ++t) cost += step_max(t);
-      atomicAdd(stats + 0, (unsigned long long)cost);
-      atomicAdd(stats + 1, (unsigned long long)ident);
-      atomicAdd(stats + 2, (unsigned long long)lb);
-      if (stats_rot) {
-        // measurement: passes of the 9 element instructions per step when block s's elements are
-        // stored rotated by (alpha s + beta) mod 9 (bank color (9 s + (k + rot) mod 9) mod 16),
-        // for every (alpha, beta); stats[3 + 9 alpha + beta], in instruction passes
-        for (int ab = 0; ab < 81; ++ab) {
-          const int al = ab / 9, be = ab % 9;
-          int c2 = 0;
-          for (int t = 0; t < NBG; ++t)
-            for (int k = 0; k < 9; ++k) {
-              uint8_t h[16];
-              for (int r = 0; r < 16; ++r) h[r] = 0;
-              int m = 0;
-              for (int q = 0; q < nl; ++q) {
-                const int sp = posv[q][pick[q][t]];
-                const int e = (k + (al * sp + be) % 9) % 9;
-                const int col = (9 * sp + e) & 15;
-                m = max(m, (int)++h[col]);
-              }
-              c2 += m;
-            }
-          atomicAdd(stats + 3 + ab, (unsigned long long)c2);
-        }
-      }
-    }
     for (int q = 0; q < nl; ++q) {
       const int part = (p0 + q) % NSPLIT;
       uint16_t v[NBG];
@@ -4709,121 +3525,18 @@ __global__ void k_plan_perm(const int64_t* __restrict__ row_start, const int64_t
   }
 }
 
-// Measurement (FA_ORDER_STATS=1c): how far a per-chunk XOR recolouring of the accumulator slots
-// (LDS position (s & ~15) | ((s & 15) ^ v_g), one 4-bit v per 16-block group g = s >> 4) flattens
-// each quarter's residue histogram. stats[84..86] += the pass bound sum over quarters before /
-// after (max(NBG, largest residue count)), quarters. One thread per chunk, positional plans.
-template <int NN, int NSPLIT>
-__global__ void k_plan_colors_stats(const int64_t* __restrict__ row_start, const int64_t* __restrict__ indptr,
-                                    const int64_t* __restrict__ adj_ptr, int64_t nchunks,
-                                    const uint16_t* __restrict__ src, const uint16_t* __restrict__ eperm,
-                                    unsigned long long* __restrict__ stats) {
-  constexpr int EQ = NSPLIT <= 16 ? 16 / NSPLIT : 1, NBG = NN / NSPLIT, MQ = kGatherMaxAdj / EQ, MG = 64;
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r0 = row_start[c], r1 = row_start[c + 1];
-    const int64_t a0 = adj_ptr[r0];
-    const int na = (int)(adj_ptr[r1] - a0);
-    if (na <= 0) continue;
-    const int64_t b0 = indptr[r0];
-    const int nq = (na + EQ - 1) / EQ;
-    if (nq > 32) continue;
-    uint8_t cnt[32][16];
-    for (int q = 0; q < nq; ++q)
-      for (int r = 0; r < 16; ++r) cnt[q][r] = 0;
-    // hits per (group, quarter, low 4 bits): gh[g][q] bitmask is not enough (counts) -> per group
-    // a list of (quarter, low bits) hits
-    uint16_t hq[kGatherMaxAdj * NN];  // packed quarter << 8 | slot (slot < 512)
-    int nh = 0;
-    for (int pos = 0; pos < na; ++pos) {
-      const int j = (int)eperm[a0 + pos];
-      const int64_t e = a0 + j;
-      int64_t lo = r0, hi = r1 - 1;
-      while (lo < hi) {
-        const int64_t mid = (lo + hi + 1) >> 1;
-        if (adj_ptr[mid] <= e) lo = mid; else hi = mid - 1;
-      }
-      const int rowlo = (int)(indptr[lo] - b0);
-      const int q = pos / EQ;
-      for (int b = 0; b < NN; ++b) {
-        const int sl = rowlo + src[e * NN + b];
-        hq[nh++] = (uint16_t)((q << 10) | sl);
-        ++cnt[q][sl & 15];
-      }
-    }
-    auto bound = [&]() {
-      int t = 0;
-      for (int q = 0; q < nq; ++q) {
-        int m = NBG;
-        for (int r = 0; r < 16; ++r) m = max(m, (int)cnt[q][r]);
-        t += m;
-      }
-      return t;
-    };
-    const int before = bound();
-    uint8_t v[MG];
-    for (int g = 0; g < MG; ++g) v[g] = 0;
-    for (int sweep = 0; sweep < 3; ++sweep) {
-      for (int g = 0; g < MG; ++g) {
-        // remove group g's hits, try the 16 XOR values, keep the one with the smallest sum of
-        // squared counts (ties: the current one)
-        bool any = false;
-        for (int k = 0; k < nh; ++k)
-          if (((hq[k] & 1023) >> 4) == g) {
-            any = true;
-            --cnt[hq[k] >> 10][(hq[k] & 15) ^ v[g]];
-          }
-        if (!any) continue;
-        int bestv = v[g];
-        long bestc = 1L << 60;
-        for (int x = 0; x < 16; ++x) {
-          long cst = 0;
-          for (int k = 0; k < nh; ++k)
-            if (((hq[k] & 1023) >> 4) == g) {
-              const int q = hq[k] >> 10, r = (hq[k] & 15) ^ x;
-              cst += 2 * cnt[q][r] + 1;  // increase of the sum of squares when adding this hit
-              ++cnt[q][r];
-            }
-          for (int k = 0; k < nh; ++k)
-            if (((hq[k] & 1023) >> 4) == g) --cnt[hq[k] >> 10][(hq[k] & 15) ^ x];
-          if (cst < bestc || (cst == bestc && x == v[g])) { bestc = cst; bestv = x; }
-        }
-        v[g] = (uint8_t)bestv;
-        for (int k = 0; k < nh; ++k)
-          if (((hq[k] & 1023) >> 4) == g) ++cnt[hq[k] >> 10][(hq[k] & 15) ^ v[g]];
-      }
-    }
-    atomicAdd(stats + 84, (unsigned long long)before);
-    atomicAdd(stats + 85, (unsigned long long)bound());
-    atomicAdd(stats + 86, (unsigned long long)nq);
-  }
-}
-
 // NSPLIT of the affine-simplex linear-elasticity gather kernel for (cell, degree, quadrature
 // points), or 0 when that kernel does not exist (must match dispatch_gather)
-#ifndef FA_P2TET_NSPLIT
-#define FA_P2TET_NSPLIT 2  // measured best with the reference-tensor blocks (n=120 sweep)
-#endif
+constexpr int FA_P2TET_NSPLIT = 2;  // measured best with the reference-tensor blocks (n=120 sweep)
 // affine tensor cells: column nodes per item = NN / NSPLIT
-#ifndef FA_Q2HEX_NSPLIT
-#define FA_Q2HEX_NSPLIT 9
-#endif
-#ifndef FA_Q3HEX_NSPLIT
-#define FA_Q3HEX_NSPLIT 32
-#endif
-#ifndef FA_Q2QUAD_NSPLIT
-#define FA_Q2QUAD_NSPLIT 3
-#endif
-#ifndef FA_P1TET_NSPLIT
-#define FA_P1TET_NSPLIT 1  // P1 tetrahedra: whole entries (4 blocks per item); config C 1.86 vs 1.97 ms (2), 2.25 (4)
-#endif
+constexpr int FA_Q2HEX_NSPLIT = 9;
+constexpr int FA_Q3HEX_NSPLIT = 32;
+constexpr int FA_Q2QUAD_NSPLIT = 3;
+constexpr int FA_P1TET_NSPLIT = 1;  // P1 tetrahedra: whole entries (4 blocks per item); config C 1.86 vs 1.97 ms (2), 2.25 (4)
 // k_gather_lin's workgroup size (one item per thread, chunks of up to NT / NSPLIT entries): P1
 // tetrahedra have 4-block items, so their chunks are short on work per barrier at 256 items
-#ifndef FA_P1TET_NT
-#define FA_P1TET_NT 256  // 512 measured 1.72 vs 1.68 ms on config C
-#endif
-#ifndef FA_P2TET_NT
-#define FA_P2TET_NT 256
-#endif
+constexpr int FA_P1TET_NT = 256;  // 512 measured 1.72 vs 1.68 ms on config C
+constexpr int FA_P2TET_NT = 256;
 __host__ __device__ constexpr int lin_threads(int gd, int nn) {
   return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : 256;
 }
@@ -4861,17 +3574,6 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   hipStream_t s = (hipStream_t)stream;
   const int64_t total = plan->nchunks * groups;
   uint16_t* sl = const_cast<uint16_t*>(plan->slots);
-  // FA_ORDER_STATS=1: print the LDS passes of the accumulate steps (ordered / identity / bound)
-  const char* ev = getenv("FA_ORDER_STATS");
-  unsigned long long* st = nullptr;
-  if (ev && ev[0] == '1') {
-    HIP_TRY(hipMallocAsync((void**)&st, 88 * sizeof(unsigned long long), s));
-    HIP_TRY(hipMemsetAsync(st, 0, 88 * sizeof(unsigned long long), s));
-  }
-  const int stats_rot = (ev && ev[0] == '1' && ev[1] == 'r') ? 1 : 0;  // FA_ORDER_STATS=1r
-  const bool stats_col = ev && ev[0] == '1' && ev[1] == 'c';              // FA_ORDER_STATS=1c
-  const char* ke = getenv("FEMASM_ORDER_KICKS");
-  const int kicks = ke ? atoi(ke) : FA_ORDER_KICKS;
   // positional plan: the plain map is copied aside (the order kernel rewrites by position). Only
   // for the kernels that read one (k_gather's POSM: an entry's items fill whole 16-lane quarters,
   // and affine tensor cells only with a full bc mask, NN * GD <= 32)
@@ -4889,12 +3591,8 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
     if (posn)                                                                                                 \
       k_plan_perm<NN_, NS_><<<grid_for(plan->nchunks), 64, 0, s>>>(plan->row_start, A->indptr, adj->ptr,      \
                                                                    adj->idx, plan->nchunks, src, eperm, eadj);   \
-    if (posn && stats_col)                                                                                    \
-      k_plan_colors_stats<NN_, NS_><<<grid_for(plan->nchunks, 64), 64, 0, s>>>(plan->row_start, A->indptr,        \
-                                                                              adj->ptr, plan->nchunks, src,     \
-                                                                              eperm, st);                       \
     k_order_slots<NN_, NS_><<<grid_for(total), 256, 0, s>>>(plan->row_start, A->indptr, adj->ptr, plan->nchunks, \
-                                                            groups, sl, src, eperm, st, kicks, stats_rot);    \
+                                                            groups, sl, src, eperm);                           \
   } while (0)
   bool ok = true;
   if (mesh->nn == 3 && ns == 1) ORD(3, 1);
@@ -4913,31 +3611,8 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
 #undef ORD
   if (src) HIP_TRY(hipFreeAsync(src, s));
   if (eperm) HIP_TRY(hipFreeAsync(eperm, s));
-  if (!ok) {
-    if (st) (void)hipFreeAsync(st, s);
-    return FA_OK;
-  }
+  if (!ok) return FA_OK;
   LAUNCH_CHECK();
-  if (st) {
-    unsigned long long h[88];
-    HIP_TRY(hipMemcpyAsync(h, st, sizeof(h), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipFreeAsync(st, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    fprintf(stderr, "fa_plan_order: LDS passes ordered %llu identity %llu bound %llu (%.3f / %.3f of identity)\n", h[0],
-            h[1], h[2], (double)h[0] / (double)h[1], (double)h[2] / (double)h[1]);
-    if (stats_col)
-      fprintf(stderr, "fa_plan_order: XOR recolouring: pass bound per quarter %.3f -> %.3f (%llu quarters)\n",
-              (double)h[84] / (double)h[86], (double)h[85] / (double)h[86], h[86]);
-    if (stats_rot) {
-      int best = 0;
-      for (int ab = 1; ab < 81; ++ab)
-        if (h[3 + ab] < h[3 + best]) best = ab;
-      fprintf(stderr, "fa_plan_order: element-rotated passes: none %.4g, best global (alpha %d, beta %d) %.4g (%.3f)\n",
-              (double)h[3] / 9.0, best / 9, best % 9, (double)h[3 + best] / 9.0, (double)h[3 + best] / (double)h[3]);
-      for (int al = 0; al < 9; ++al)
-        fprintf(stderr, "  alpha %d: %.4f\n", al, (double)h[3 + 9 * al] / (double)h[3]);
-    }
-  }
   HIP_TRY(hipStreamSynchronize(s));
   plan->slot_order = ns;
   plan->eadj = posn ? eadj : nullptr;
@@ -5040,7 +3715,6 @@ static int plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bs
   return FA_OK;
 }
 
-static bool lin_gather_enabled();
 extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int64_t* row_start,
                               fa_plan* plan, void* stream) {
   if (!mesh) return fail(FA_E_ARG, "null mesh");
@@ -5052,7 +3726,7 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
     int rc = get_tables(mesh->cell_type, mesh->degree, -1, &T);
     if (rc) return rc;
     const int ns = lin_simplex_nsplit(mesh->cell_type, mesh->degree, T.nq);
-    if (ns > 0 && lin_gather_enabled()) maxadj = std::min(maxadj, lin_threads(mesh->gdim, mesh->nn) / ns);
+    if (ns > 0) maxadj = std::min(maxadj, lin_threads(mesh->gdim, mesh->nn) / ns);
   }
   return plan_gather(mesh, adj, A, row_start, plan, stream, gather_maxb(false, mesh->gdim * mesh->gdim), maxadj);
 }
@@ -5461,30 +4135,18 @@ __global__ void k_chunk_desc(const int64_t* __restrict__ row_start, int64_t nchu
   }
 }
 
-static bool gather_dynamic() {
-  const char* e = getenv("FEMASM_GATHER_SCHED");
-  return !(e && strcmp(e, "static") == 0);
-}
-
 // k_gather_lin's grid: about FA_LIN_CHUNKS_PER_WG chunks per workgroup, never fewer workgroups than
 // are resident. A grid many times the resident count lets the dispatcher balance the chunks' uneven
 // cost across CUs and XCDs: config E 44.5 ms at the resident count (~4,700 chunks per workgroup),
 // 43.7 / 42.8 / 41.7 / 40.3 / 39.5 ms at 2 / 4 / 8 / 32 / 128 times it, 44.6 ms at 1024 times (~5 per
 // workgroup); config C (162 k chunks) best at 4-8 times (1.30 vs 1.34 ms), 1.46 at 32 times.
-// FEMASM_GATHER_GRID_MULT keeps the resident-count grid times its value (measurement knob).
-#ifndef FA_LIN_CHUNKS_PER_WG
-#define FA_LIN_CHUNKS_PER_WG 32
-#endif
-// k_gather_neo likewise, at ~FA_NEO_CHUNKS_PER_WG (config E-neo, alternating on one box: 74.0-74.3 ms
+constexpr int kLinChunksPerWg = 32;
+// k_gather_neo likewise, at ~kNeoChunksPerWg (config E-neo, alternating on one box: 74.0-74.3 ms
 // at 64 times the resident count against 75.5-76.9 at 1 time)
-#ifndef FA_NEO_CHUNKS_PER_WG
-#define FA_NEO_CHUNKS_PER_WG 128
-#endif
+constexpr int kNeoChunksPerWg = 128;
 template <typename K>
-static int64_t lin_grid(K kernel, int64_t nchunks, int block, int per_wg = FA_LIN_CHUNKS_PER_WG) {
+static int64_t lin_grid(K kernel, int64_t nchunks, int block, int per_wg = kLinChunksPerWg) {
   const int64_t g0 = gather_grid(kernel, nchunks, block);
-  const char* env = getenv("FEMASM_GATHER_GRID_MULT");
-  if ((env && atof(env) > 0) || !gather_dynamic()) return g0;
   const int64_t per = (nchunks + 7) / 8;
   const int64_t g = std::max<int64_t>(g0, nchunks / per_wg / 8 * 8);
   return std::min<int64_t>(std::min<int64_t>(8 * per, g), kMaxBlocks);
@@ -5496,11 +4158,8 @@ static int chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
   if ((rc = scratch_alloc((void**)buf, sizeof(int64_t) * (2 * (P.nchunks + 1) + 8), s))) return rc;
   P.chunk_b = *buf;
   P.chunk_a = *buf + (P.nchunks + 1);
-  P.ctr = nullptr;
-  if (gather_dynamic()) {
-    P.ctr = reinterpret_cast<unsigned long long*>(*buf + 2 * (P.nchunks + 1));
-    HIP_TRY(hipMemsetAsync(P.ctr, 0, 8 * sizeof(unsigned long long), s));
-  }
+  P.ctr = reinterpret_cast<unsigned long long*>(*buf + 2 * (P.nchunks + 1));
+  HIP_TRY(hipMemsetAsync(P.ctr, 0, 8 * sizeof(unsigned long long), s));
   k_chunk_desc<<<grid_for(P.nchunks + 1), 256, 0, s>>>(P.row_start, P.nchunks, P.A.indptr, P.adj_ptr, *buf,
                                                       *buf + (P.nchunks + 1));
   LAUNCH_CHECK();
@@ -5511,22 +4170,18 @@ static int chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
 // occupancy, a multiple of 8 for the XCD order), each workgroup pulling chunks from its XCD's
 // counter with three chunks of look-ahead, so chunk k's stores, chunk k+1's metadata loads and
 // the per-workgroup LDS tables overlap the work instead of heading every chunk (measured on
-// config E: skeleton 41.9 -> 33.0 ms persistent). FEMASM_GATHER_SCHED=static: one workgroup per
-// chunk (capped below the 2^32 work-item limit; larger plans loop). FEMASM_GATHER_GRID_MULT=m
-// scales the persistent grid (measurement knob).
+// config E: skeleton 41.9 -> 33.0 ms persistent; a static grid of one workgroup per chunk, and
+// larger persistent grids, measured slower).
 template <typename K>
 static int64_t gather_grid(K kernel, int64_t nchunks, int block = 256) {
   const int64_t per = (nchunks + 7) / 8;
-  const char* env = getenv("FEMASM_GATHER_GRID_MULT");
-  if (!gather_dynamic()) return std::min<int64_t>(8 * per, kMaxBlocks);  // kMaxBlocks % 8 == 0
   int dev = 0, cus = 256, occ = 4;
   if (hipGetDevice(&dev) == hipSuccess) {
     int v = 0;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kernel, block, 0) == hipSuccess && v > 0) occ = v;
   }
-  const double mult = (env && atof(env) > 0) ? atof(env) : 1.0;
-  int64_t g = (int64_t)(cus * occ * mult);
+  int64_t g = (int64_t)cus * occ;
   g = std::max<int64_t>(8, g / 8 * 8);
   return std::min<int64_t>(std::min<int64_t>(8 * per, g), kMaxBlocks);  // kMaxBlocks % 8 == 0
 }
@@ -5562,12 +4217,6 @@ __global__ void k_bhat(const double* __restrict__ ahat, int nblk, double r, doub
         bhat[t * GD * GD + i * GD + k] = r * ahat[t * GD * GD + i * GD + k] + ahat[t * GD * GD + k * GD + i];
 }
 
-// FEMASM_LIN_GATHER=0: the affine-simplex elasticity plans run k_gather instead of k_gather_lin
-static bool lin_gather_enabled() {
-  const char* e = getenv("FEMASM_LIN_GATHER");
-  return !(e && e[0] == '0');
-}
-
 // k_gather_lin's constant operands: a zero mask word (no bcs) and a scratch line for the stores of
 // a chunk without values; allocated once per process
 static int lin_scratch(uint32_t** zero32, double** dump) {
@@ -5587,10 +4236,12 @@ static int lin_scratch(uint32_t** zero32, double** dump) {
   return FA_OK;
 }
 
-// FEMASM_NEO_M=0: neo-Hookean simplices run k_gather's neo items (tiled C records) instead of k_gather_neo
-static bool neo_m_enabled() {
-  const char* e = getenv("FEMASM_NEO_M");
-  return !(e && e[0] == '0');
+// FIX bound constant of k_gather_lin: |block entry| <= fixc * rho^2, rho = sum |s Ji| of the record.
+// P1 blocks (from the record's gradients g, |g_i| <= rho): cv (|r| g_a g_b^T + g_b g_a^T + (g_a.g_b) I);
+// table blocks: (s Ji)^T B (s Ji) + tr / (1 + r) I with |B| <= (|r| + 1) amax
+static double lin_fix_bound(int gd, int nn, double rlm, double trc, double amax) {
+  if (nn == gd + 1) return (gd == 2 ? 0.5 : 1.0 / 6.0) * (std::fabs(rlm) + 1.0 + gd);
+  return (std::fabs(rlm) + 1.0) * amax * (1.0 + gd * std::fabs(trc));
 }
 
 static bool neo_m_plan_ok(const GatherArgs& P, int nsplit) {
@@ -5607,10 +4258,11 @@ static int launch_gather_neo(GatherArgs P, const int8_t* bc, hipStream_t s, cons
     return FA_OK;
   }
   const bool rows = P.nchunks > 0 && W.mode != GatherStage::PREP;
+  if (rows && P.fix) return fail(FA_E_UNSUPPORTED, "deterministic assembly: not for the neo-Hookean gather");
   if (rows) {  // the kernel's plan: positional, ordered for NSPLIT, <= 256 items per chunk
     if (!neo_m_plan_ok(P, NSPLIT))
       return fail(FA_E_ARG, "the neo-Hookean gather needs a positional plan ordered for %d column parts with <= %d "
-                  "entries per chunk (fa_plan_gather_form + fa_plan_slots + fa_plan_order), or FEMASM_NEO_M=0",
+                  "entries per chunk (fa_plan_gather_form + fa_plan_slots + fa_plan_order with an entry buffer)",
                   NSPLIT, 256 / NSPLIT);
     if (P.plan_maxb > gather_maxb(true, GD * GD))
       return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, the kernel %d: plan with fa_plan_gather_form",
@@ -5637,9 +4289,8 @@ static int launch_gather_neo(GatherArgs P, const int8_t* bc, hipStream_t s, cons
     uint32_t* zero32 = nullptr;
     double* dump = nullptr;
     if ((rc = lin_scratch(&zero32, &dump))) return rc;
-    constexpr int QS = neo_qsplit<NQ>();
-    const int64_t grid = lin_grid(k_gather_neo<GD, NN, NQ, NSPLIT, QS>, P.nchunks, 256 * QS, FA_NEO_CHUNKS_PER_WG);
-    k_gather_neo<GD, NN, NQ, NSPLIT, QS><<<(unsigned)grid, 256 * QS, 0, s>>>(P, zero32, dump);
+    const int64_t grid = lin_grid(k_gather_neo<GD, NN, NQ, NSPLIT>, P.nchunks, 256, kNeoChunksPerWg);
+    k_gather_neo<GD, NN, NQ, NSPLIT><<<(unsigned)grid, 256, 0, s>>>(P, zero32, dump);
     LAUNCH_CHECK();
     if (bc) {  // Dirichlet diagonals (dolfinx set_diagonal) of the plan's rows
       k_bc_diag<GD><<<grid_for((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
@@ -5653,12 +4304,17 @@ static int launch_gather_neo(GatherArgs P, const int8_t* bc, hipStream_t s, cons
   return FA_OK;
 }
 
-template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT, int VAR = 0>
+template <int GD, int NN, int NV, int NQ, int NSPLIT, int MAT>
 static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const GatherStage& W) {
   using R = Rec<GD, NV, NQ, MAT>;
+  if constexpr (MAT == FA_NEO_HOOKEAN) {
+    // the neo-Hookean M gather (k_gather_neo) and its records; its plans must be positional
+    static_assert(R::SIMP && NN % NSPLIT == 0 && NN * GD <= 32 && NN < 64, "neo-Hookean gather: simplices");
+    return launch_gather_neo<GD, NN, NQ, NSPLIT>(P, bc, s, W);
+  } else {
   // ordered (packed) slots are read only by the affine-simplex linear kernel of the same NSPLIT;
   // any other kernel searches its slots in LDS instead
-  if (P.slot_order && !((MAT == 0 || MAT == MAT_LINU || MAT == MAT_AFFT || MAT == FA_NEO_HOOKEAN) && R::SIMP &&
+  if (P.slot_order && !((MAT == 0 || MAT == MAT_LINU || MAT == MAT_AFFT) && R::SIMP &&
                         NN % NSPLIT == 0 && P.slot_order == NSPLIT)) {
     P.slots = nullptr;
     P.slot_order = 0;
@@ -5666,35 +4322,25 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   }
   // a positional plan's slot map is by position: a kernel without positional items (k_gather's
   // POSM) cannot read it -- search the slots in LDS instead
-  constexpr bool POSM_K = (MAT == 0 || MAT == MAT_LINU || (MAT == MAT_AFFT && NN * GD <= 32) || MAT == FA_NEO_HOOKEAN) &&
-                          R::SIMP && NN % NSPLIT == 0;
+  constexpr bool POSM_K = (MAT == 0 || MAT == MAT_LINU || (MAT == MAT_AFFT && NN * GD <= 32)) && R::SIMP &&
+                          NN % NSPLIT == 0;
   if (P.eadj && !POSM_K) {
     P.slots = nullptr;
     P.slot_order = 0;
     P.eadj = nullptr;
   }
   static_assert(NN * GD <= 32 || MAT == MAT_AFFT, "bc mask holds 32 dofs");
-  if (P.plan_maxb > gather_maxb(MAT == FA_NEO_HOOKEAN, GD * GD))
+  if (P.plan_maxb > gather_maxb(false, GD * GD))
     return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, this form's kernel %d: plan with fa_plan_gather_form",
-                P.plan_maxb, gather_maxb(MAT == FA_NEO_HOOKEAN, GD * GD));
-  // locality order: pays where the records are large (neo-Hookean tangents, 1.5 KB per cell:
+                P.plan_maxb, gather_maxb(false, GD * GD));
+  // the chunk visiting order (fa_plan_locality) pays where the records are large (neo-Hookean,
   // 342 -> 328 ms on config E-neo); the 80-B linear records stay in L2 in row order (E: 50.0 vs
-  // 51.5 ms in Morton order). FEMASM_CHUNK_ORDER_ALL=1 applies it to every kernel.
-  {
-    const char* e = getenv("FEMASM_CHUNK_ORDER_ALL");
-    if (MAT != FA_NEO_HOOKEAN && !(e && e[0] == '1')) P.corder = nullptr;
-  }
-  if constexpr (MAT == FA_NEO_HOOKEAN && R::SIMP && NN % NSPLIT == 0 && NN * GD <= 32 && NN < 64) {
-    // the neo-Hookean M gather (k_gather_neo) and its records: chosen per process (FEMASM_NEO_M=0
-    // keeps k_gather's neo items), since the prepare stage of the split ABI has no plan
-    // fa_assemble_matrix (both stages here) with a plan the M gather cannot run keeps k_gather's items
-    if (neo_m_enabled() && (W.mode != GatherStage::FULL || neo_m_plan_ok(P, NSPLIT)))
-      return launch_gather_neo<GD, NN, NQ, NSPLIT>(P, bc, s, W);
-  }
+  // 51.5 ms in Morton order)
+  P.corder = nullptr;
   if constexpr (MAT == MAT_LINU && R::SIMP && NN == GD + 1 && NN % NSPLIT == 0 && FA_LIN_FUSE) {
     // P1 simplices through fa_assemble_matrix: k_gather_lin forms the records itself (FUSE)
     constexpr int LNT = lin_threads(GD, NN);
-    if (W.mode == GatherStage::FULL && P.nchunks > 0 && P.F.E && !P.cw && lin_gather_enabled() && P.eadj &&
+    if (W.mode == GatherStage::FULL && P.nchunks > 0 && P.F.E && !P.cw && P.eadj &&
         P.slots && P.slot_order == NSPLIT && !P.corder && P.plan_maxadj * NSPLIT <= LNT && P.plan_maxadj >= 0 &&
         P.plan_maxb <= gather_maxb(false, GD * GD) && P.nchunks < (1ll << 31)) {
       int rc;
@@ -5714,9 +4360,14 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       double* dump = nullptr;
       if ((rc = lin_scratch(&zero32, &dump))) return rc;
       if (!nm) P.nodemask = reinterpret_cast<const uint8_t*>(zero32);  // a valid address (mask scaled by 0)
-      const int64_t grid = lin_grid(k_gather_lin<GD, NN, NSPLIT, LNT, true>, P.nchunks, LNT);
-      const int64_t per = (P.nchunks + grid - 1) / grid;
-      k_gather_lin<GD, NN, NSPLIT, LNT, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, per);
+      P.fixc = lin_fix_bound(GD, NN, P.rlm, P.trc, P.amax);
+      if (P.fix) {
+        const int64_t grid = lin_grid(k_gather_lin<GD, NN, NSPLIT, LNT, true, true>, P.nchunks, LNT);
+        k_gather_lin<GD, NN, NSPLIT, LNT, true, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
+      } else {
+        const int64_t grid = lin_grid(k_gather_lin<GD, NN, NSPLIT, LNT, true>, P.nchunks, LNT);
+        k_gather_lin<GD, NN, NSPLIT, LNT, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
+      }
       LAUNCH_CHECK();
       if (bc) {
         k_bc_diag<GD><<<grid_for((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
@@ -5743,8 +4394,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     mask = bc ? reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.work) + rec_bytes) : nullptr;
   }
   if (nc > 0 && W.mode != GatherStage::ROWS) {
-    if constexpr (R::TILED) k_neo_records_tiled<GD, NN, NV, NQ><<<grid_for(nc), 256, 0, s>>>(P.M, P.F, P.tab, bc, rec, mask);
-    else if constexpr (R::SIZE <= 16 && MAT != FA_NEO_HOOKEAN && FA_REC_STAGED)
+    if constexpr (R::SIZE <= 16)  // small records: stored through LDS as contiguous runs
       k_cell_records_staged<GD, NN, NV, NQ, MAT><<<grid_for(nc), 256, 0, s>>>(P.M, P.F, P.tab, bc, rec, mask);
     else k_cell_records<GD, NN, NV, NQ, MAT><<<grid_for(nc), 256, 0, s>>>(P.M, P.F, P.tab, bc, rec, mask);
     LAUNCH_CHECK();
@@ -5754,7 +4404,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   if constexpr (MAT == MAT_LINU && R::SIMP && NN % NSPLIT == 0 && NN * GD <= 32 && NN < 64) {
     // the store-decoupled gather (k_gather_lin): positional plans of <= 256 items per chunk
     constexpr int LNT = lin_threads(GD, NN);
-    if (P.nchunks > 0 && W.mode != GatherStage::PREP && !P.cw && lin_gather_enabled() && P.eadj && P.slots &&
+    if (P.nchunks > 0 && W.mode != GatherStage::PREP && !P.cw && P.eadj && P.slots &&
         P.slot_order == NSPLIT && !P.corder && P.plan_maxadj * NSPLIT <= LNT && P.plan_maxadj >= 0) {
       if (P.plan_maxb > gather_maxb(false, GD * GD))
         return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, the kernel %d", P.plan_maxb,
@@ -5771,9 +4421,14 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       uint32_t* zero32 = nullptr;
       double* dump = nullptr;
       if ((rc = lin_scratch(&zero32, &dump))) return rc;
-      const int64_t grid = lin_grid(k_gather_lin<GD, NN, NSPLIT, LNT>, P.nchunks, LNT);
-      const int64_t per = (P.nchunks + grid - 1) / grid;
-      k_gather_lin<GD, NN, NSPLIT, LNT><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, per);
+      P.fixc = lin_fix_bound(GD, NN, rr, P.trc, P.amax);
+      if (P.fix) {
+        const int64_t grid = lin_grid(k_gather_lin<GD, NN, NSPLIT, LNT, false, true>, P.nchunks, LNT);
+        k_gather_lin<GD, NN, NSPLIT, LNT, false, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
+      } else {
+        const int64_t grid = lin_grid(k_gather_lin<GD, NN, NSPLIT, LNT>, P.nchunks, LNT);
+        k_gather_lin<GD, NN, NSPLIT, LNT><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
+      }
       LAUNCH_CHECK();
       if (bc) {  // Dirichlet diagonals (dolfinx set_diagonal) of the plan's rows
         k_bc_diag<GD><<<grid_for((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
@@ -5788,9 +4443,12 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     }
   }
   if (P.nchunks > 0 && W.mode != GatherStage::PREP) {
+    if (P.fix)
+      return fail(FA_E_UNSUPPORTED, "deterministic assembly runs the affine-simplex elasticity gather (uniform nu, "
+                                    "positional plan: fa_plan_slots + fa_plan_order with an entry buffer) only");
     int64_t* desc = nullptr;
     if ((rc = chunk_desc(P, &desc, s))) return rc;
-    const int64_t grid = gather_grid(k_gather<GD, NN, NV, NQ, NSPLIT, MAT, VAR>, P.nchunks);
+    const int64_t grid = gather_grid(k_gather<GD, NN, NV, NQ, NSPLIT, MAT>, P.nchunks);
     double* bhat = nullptr;
     if constexpr (MAT == MAT_AFFT) {  // the kernel forms B_ab = r Ahat_ab + Ahat_ab^T per block
       const double nu = P.F.nu;
@@ -5806,61 +4464,18 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       P.trc = 1.0 / (1.0 + rr);
       P.rlm = rr;
     }
-#if FA_GATHER_TIMING
-    {
-      unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-      HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_gather_timing), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
-    }
-#endif
     bool launched = false;
     if constexpr (MAT == MAT_LINU && Rec<GD, NV, NQ, MAT>::SIMP && NN * GD <= 32 && NN * NN < 127) {
       if (P.cw) {  // contribution plan: the block-owner gather
         if (P.plan_maxb > own_maxb(GD * GD))
           return fail(FA_E_ARG, "contribution plan chunks hold %d blocks, the kernel %d", P.plan_maxb, own_maxb(GD * GD));
         const int64_t go = gather_grid(k_gather_own<GD, NN>, P.nchunks);
-#if FA_OWN_TIMING
-        {
-          unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-          HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_gather_timing), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
-        }
-#endif
         k_gather_own<GD, NN><<<(unsigned)go, 256, 0, s>>>(P);
         launched = true;
-#if FA_OWN_TIMING
-        {
-          unsigned long long t[10];
-          HIP_TRY(hipMemcpyFromSymbolAsync(t, HIP_SYMBOL(g_gather_timing), sizeof(t), 0, hipMemcpyDeviceToHost, s));
-          HIP_TRY(hipStreamSynchronize(s));
-          const double n = (double)(t[6] ? t[6] : 1);
-          fprintf(stderr, "[own timing] per wave-chunk (s_memtime): loop %.0f | B2 %.0f | atomics+stage %.0f | B3 %.0f | "
-                          "store %.0f | B1 %.0f | wave-chunks %llu\n", t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n,
-                  t[5] / n, t[6]);
-        }
-#endif
       }
     }
-    if constexpr (MAT == MAT_LINU && Rec<GD, NV, NQ, MAT>::SIMP && Bary<GD, NN>::NPART == NSPLIT &&
-                  Bary<GD, NN>::NB == (NN + NSPLIT - 1) / NSPLIT && FA_GATHER_BARY && FA_ABL == 0) {
-      if (P.slots && !P.slot_order) {  // barycentric blocks read the plain slot map
-        const int64_t gb = gather_grid(k_gather<GD, NN, NV, NQ, NSPLIT, MAT, 1>, P.nchunks);
-        k_gather<GD, NN, NV, NQ, NSPLIT, MAT, 1><<<(unsigned)gb, 256, 0, s>>>(P);
-        launched = true;
-      }
-    }
-    if (!launched) k_gather<GD, NN, NV, NQ, NSPLIT, MAT, VAR><<<(unsigned)grid, 256, 0, s>>>(P);
+    if (!launched) k_gather<GD, NN, NV, NQ, NSPLIT, MAT><<<(unsigned)grid, 256, 0, s>>>(P);
     LAUNCH_CHECK();
-#if FA_GATHER_TIMING
-    {
-      unsigned long long t[10];
-      HIP_TRY(hipMemcpyFromSymbolAsync(t, HIP_SYMBOL(g_gather_timing), sizeof(t), 0, hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipStreamSynchronize(s));
-      const double n = (double)(t[6] ? t[6] : 1);
-      fprintf(stderr, "[gather timing] per wave-chunk (shader clocks): items %.0f | wait-items %.0f | store %.0f | "
-                      "wait-store %.0f | stage %.0f | wait-stage %.0f | wave-chunks %llu | item loads %.0f | "
-                      "item blocks %.0f | store: meta staging %.0f\n",
-              t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5] / n, t[6], t[7] / n, t[8] / n, t[9] / n);
-    }
-#endif
     HIP_TRY(hipFreeAsync(desc, s));
     if (bhat) HIP_TRY(hipFreeAsync(bhat, s));
   }
@@ -5869,12 +4484,9 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     if (mask) HIP_TRY(hipFreeAsync(mask, s));
   }
   return FA_OK;
+  }
 }
 
-#ifndef FA_NEO_NSPLIT
-#define FA_NEO_NSPLIT 2  // column items of 5 columns sharing each tangent sub-block load; config E-neo at
-                         // 2 waves / SIMD: 342 ms (NSPLIT 5 at 3 waves 349, 10 at 4 waves 461)
-#endif
 // Hexahedra: MFMA element blocks into a stream-ordered block store, then the row gather sums
 // them (the "store pass + per-destination sum pass" alternative to global atomics).
 template <int NN, int NQ, int NSPLIT>
@@ -5906,6 +4518,7 @@ static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc,
   P.rec = eb;
   P.bcmask = nullptr;
   if (P.nchunks > 0 && W.mode != GatherStage::PREP) {
+    if (P.fix) return fail(FA_E_UNSUPPORTED, "deterministic assembly: not for non-affine hexahedra");
     int64_t* desc = nullptr;
     if ((rc = chunk_desc(P, &desc, s))) return rc;
     const int64_t grid = gather_grid(k_gather<3, NN, 8, NQ, NSPLIT, MAT_BLOCKS>, P.nchunks);
@@ -5918,10 +4531,7 @@ static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc,
 }
 
 // the uniform-nu affine-simplex kernels (MAT_LINU): E per cell with one nu, away from nu = 1/2
-// (FEMASM_LINU=0: the general lam / mu kernel, a measurement knob)
 static bool lin_uniform_nu(const FormView& F) {
-  const char* e = getenv("FEMASM_LINU");
-  if (e && e[0] == '0') return false;
   return F.kind == FA_LINEAR_ELASTICITY && F.E && F.nu > -0.99 && F.nu < 0.49;
 }
 
@@ -6016,8 +4626,8 @@ extern "C" int fa_tabulate_cells(const fa_mesh* mesh, const fa_form* form, int64
   return launch_cell_blocks(0, mesh, M, F, T, c0, ncells_out, Ae, A, nullptr, nullptr, (hipStream_t)stream);
 }
 
-// Error flags raised by kernels are read back only on the checked path (FA_CHECK env or
-// scatter/gather tests); the timed path stays asynchronous.
+// Error flags raised by kernels (a pattern entry or diagonal the mesh needs is missing) are read
+// back only with FA_CHECK_ERRORS, which synchronises the stream; the timed path stays asynchronous.
 extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, const fa_adjacency* adj, const fa_plan* plan,
                                   const int8_t* bc, double diag, fa_bsr* A, int32_t flags, void* stream) {
   int rc = check_mesh(mesh);
@@ -6052,10 +4662,14 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr; P.nodemask = nullptr;
     P.affine = (plan->cell_flags & FA_PLAN_AFFINE) != 0;
     P.t1d = T.t1d; P.lat = T.lat;
+    P.fix = ((flags & FA_DETERMINISTIC) || (plan->cell_flags & FA_PLAN_DETERMINISTIC)) ? 1 : 0;
+    P.amax = T.amax;
     set_contrib(P, plan);
+    if (P.fix && P.cw) return fail(FA_E_UNSUPPORTED, "deterministic assembly: not with a contribution plan");
     bool handled = false;
     rc = dispatch_gather(mesh, T, F.kind, P, bc, s, &handled);
     if (rc) return rc;
+    if (!handled && P.fix) return fail(FA_E_UNSUPPORTED, "deterministic assembly: no gather kernel for this form");
     if (!handled) scatter = true;  // no specialised gather kernel: generic element scatter
   }
   if (scatter) {
@@ -6078,7 +4692,7 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
       LAUNCH_CHECK();
     }
   }
-  if (getenv("FA_CHECK")) {
+  if (flags & FA_CHECK_ERRORS) {
     int herr = 0;
     HIP_TRY(hipMemcpyAsync(&herr, derr, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -6128,7 +4742,10 @@ static int gather_stage(const fa_mesh* mesh, const fa_form* form, const fa_adjac
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;
+    P.fix = (plan->cell_flags & FA_PLAN_DETERMINISTIC) ? 1 : 0;
+    P.amax = T.amax;
     set_contrib(P, plan);
+    if (P.fix && P.cw) return fail(FA_E_UNSUPPORTED, "deterministic assembly: not with a contribution plan");
   }
   bool handled = false;
   rc = dispatch_gather(mesh, T, F.kind, P, bc, s, &handled, W);

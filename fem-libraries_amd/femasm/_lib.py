@@ -16,8 +16,8 @@ CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 FA_OK = 0
 FA_TRIANGLE, FA_QUADRILATERAL, FA_TETRAHEDRON, FA_HEXAHEDRON = 3, 4, -4, 8
 FA_LINEAR_ELASTICITY, FA_ASYM_DAMAGE, FA_NEO_HOOKEAN, FA_ASYM_DAMAGE_AD = 0, 1, 2, 3
-FA_GATHER, FA_SCATTER, FA_ZERO_FIRST = 0x0, 0x1, 0x2
-FA_PLAN_AFFINE = 0x1
+FA_GATHER, FA_SCATTER, FA_ZERO_FIRST, FA_DETERMINISTIC, FA_CHECK_ERRORS = 0x0, 0x1, 0x2, 0x4, 0x8
+FA_PLAN_AFFINE, FA_PLAN_DETERMINISTIC = 0x1, 0x2
 
 
 class FemasmError(RuntimeError):

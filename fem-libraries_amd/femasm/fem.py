@@ -12,7 +12,6 @@ CPU fallback.
 from __future__ import annotations
 
 import ctypes
-import os
 import weakref
 from dataclasses import dataclass
 
@@ -520,16 +519,17 @@ def _fa_bsr(A: MatrixCSR, part: int = 0) -> _lib.fa_bsr:
     return A._fa_bsr(part)
 
 
-def _plan_order(V, fm, adj, fb, plan, sh, eadj=None):
-    """Bank-conflict-aware LDS order of the affine-simplex gather (fa_plan_order). FEMASM_SLOT_ORDER:
-    "pos" (default) also balances which entries share a 16-lane quarter (positional plan, one int32
-    per adjacency entry), "1" orders each lane's blocks only, "0" keeps the plain slot map."""
-    mode = os.environ.get("FEMASM_SLOT_ORDER", "pos")
-    if mode == "0":
+def _plan_order(V, fm, adj, fb, plan, sh, eadj=None, order: str = "positional"):
+    """Bank-conflict-aware LDS order of the affine-simplex gather (fa_plan_order). order:
+    "positional" (default) also balances which entries share a 16-lane quarter (one int32 per
+    adjacency entry), "steps" orders each lane's blocks only, "none" keeps the plain slot map."""
+    if order not in ("positional", "steps", "none"):
+        raise ValueError(f"unknown slot order {order!r}")
+    if order == "none":
         return None
-    if mode == "pos" and eadj is None:
+    if order == "positional" and eadj is None:
         eadj = torch.empty(V.mesh.num_cells * V.nn, dtype=torch.int32, device=V.mesh.device)
-    if mode != "pos":
+    if order != "positional":
         eadj = None
     _lib.check(_lib.load().fa_plan_order(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb),
                                          eadj.data_ptr() if eadj is not None else None, ctypes.byref(plan), sh),
@@ -537,11 +537,11 @@ def _plan_order(V, fm, adj, fb, plan, sh, eadj=None):
     return eadj if plan.eadj else None
 
 
-def _plan_locality(V, fm, adj, plan, sh):
+def _plan_locality(V, fm, adj, plan, sh, locality: bool = True):
     """Chunk visiting order of the gather (fa_plan_locality): Morton order of the chunks' positions,
     so chunks that share cells run close in time and the cells' records are re-read from L2, not
-    HBM. FEMASM_CHUNK_ORDER=0 keeps row order."""
-    if os.environ.get("FEMASM_CHUNK_ORDER", "morton") == "0" or plan.nchunks <= 1:
+    HBM. locality=False keeps row order."""
+    if not locality or plan.nchunks <= 1:
         return None
     corder = torch.empty(plan.nchunks, dtype=torch.int32, device=V.mesh.device)
     _lib.check(_lib.load().fa_plan_locality(ctypes.byref(fm), ctypes.byref(adj), corder.data_ptr(),
@@ -549,15 +549,14 @@ def _plan_locality(V, fm, adj, plan, sh):
     return corder if plan.corder else None
 
 
-def _use_contrib(V, kind) -> bool:
+def _use_contrib(V, kind, owner) -> bool:
     """Block-owner gather (fa_plan_contrib) for linear elasticity on P1/P2 triangles and
-    tetrahedra. FEMASM_CONTRIB: "auto" (default) uses it for triangles, where it measured faster
-    (config A 0.136 vs 0.220 ms), and keeps the LDS-atomic gather for tetrahedra, where that one
-    is faster (C 1.72 vs 2.07 ms, E 46.8 vs 53.1 ms); "1" / "0" force it."""
-    mode = os.environ.get("FEMASM_CONTRIB", "auto")
-    if mode == "0" or kind != _lib.FA_LINEAR_ELASTICITY or V.degree not in (1, 2):
+    tetrahedra. owner=None (default) uses it for triangles, where it measured faster (config A
+    0.136 vs 0.220 ms), and keeps the LDS-atomic gather for tetrahedra, where that one is faster
+    (C 1.72 vs 2.07 ms, E 46.8 vs 53.1 ms); True / False force it."""
+    if owner is False or kind != _lib.FA_LINEAR_ELASTICITY or V.degree not in (1, 2):
         return False
-    if mode == "1":
+    if owner:
         return V.mesh.cell_type in (_lib.FA_TRIANGLE, _lib.FA_TETRAHEDRON)
     return V.mesh.cell_type == _lib.FA_TRIANGLE
 
@@ -584,14 +583,19 @@ def _plan_contrib(V, fm, adj, fb, rs, plan, sh):
     return buf
 
 
-def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.FA_LINEAR_ELASTICITY):
+def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.FA_LINEAR_ELASTICITY,
+                deterministic: bool = False, owner: bool | None = None, slots: bool = True,
+                order: str = "positional", locality: bool = True):
     """Row-chunk plan of the gather kernel of a form kind for one row part of A's pattern (cached
-    on V). Neo-Hookean forms get their own chunking (fa_plan_gather_form); the other kinds share one."""
+    on V per options). Neo-Hookean forms get their own chunking (fa_plan_gather_form); the other
+    kinds share one. deterministic: the LDS-atomic gather's plan (no contribution plan), for
+    FA_DETERMINISTIC. owner: the block-owner contribution plan (None: for triangles). slots: the
+    per-entry slot map (fa_plan_slots; False: the kernels search the pattern in LDS). order: the
+    slot map's LDS order (_plan_order). locality: Morton chunk order (fa_plan_locality)."""
     plans = V.__dict__.setdefault("_plans", {})
     neo = kind == _lib.FA_NEO_HOOKEAN
-    contrib = _use_contrib(V, kind)
-    key = (A.indptr.data_ptr(), A.parts[part][0], A.parts[part][1]) + (("neo",) if neo else ()) + \
-        (("contrib",) if contrib else ())
+    contrib = _use_contrib(V, kind, owner) and not deterministic
+    key = (A.indptr.data_ptr(), A.parts[part][0], A.parts[part][1], neo, contrib, slots, order, locality)
     if key not in plans:
         L = _lib.load()
         fm = V._fa_mesh()
@@ -607,21 +611,20 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.
                 return plan
         _lib.check(L.fa_plan_gather_form(ctypes.byref(fm), int(kind), ctypes.byref(adj), ctypes.byref(fb),
                                          rs.data_ptr(), ctypes.byref(plan), sh), "fa_plan_gather_form")
-        slots = eadj = None
-        mode = os.environ.get("FEMASM_SLOTS", "auto")
+        smap = eadj = None
         # Per (adjacency entry, column node) block position in its row: no LDS search in the
         # kernel, for 2 B x nn^2 extra reads per cell. Measured with the interleaved-search
         # kernel: config E 64.5 -> 61.0 ms, C 2.22 -> 2.15 ms, Q2 quads +21 % (profiles/r1/
-        # slots.md) -> on by default; FEMASM_SLOTS=0 keeps the in-kernel LDS search.
-        if mode in ("1", "auto"):
-            slots = torch.empty(V.mesh.num_cells * V.nn * V.nn, dtype=torch.int16, device=V.mesh.device)
-            _lib.check(L.fa_plan_slots(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), slots.data_ptr(),
+        # slots.md) -> on by default.
+        if slots:
+            smap = torch.empty(V.mesh.num_cells * V.nn * V.nn, dtype=torch.int16, device=V.mesh.device)
+            _lib.check(L.fa_plan_slots(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), smap.data_ptr(),
                                        ctypes.byref(plan), sh), "fa_plan_slots")
             # bank-balanced positional order of the LDS adds (affine-simplex elasticity and, with the
             # same column split, the neo-Hookean gather)
-            eadj = _plan_order(V, fm, adj, fb, plan, sh)
-        corder = _plan_locality(V, fm, adj, plan, sh)
-        plans[key] = (plan, rs, A.indptr, slots, eadj, corder)
+            eadj = _plan_order(V, fm, adj, fb, plan, sh, order=order)
+        corder = _plan_locality(V, fm, adj, plan, sh, locality)
+        plans[key] = (plan, rs, A.indptr, smap, eadj, corder)
         V.__dict__.setdefault("_plan_xver", {})[key] = _coords_version(V.mesh)
     plan = plans[key][0]
     _recheck_affine(V, key, plan)
@@ -648,12 +651,17 @@ def _recheck_affine(V: FunctionSpace, key, plan):
     vers[key] = now
 
 
-def assemble_matrix(a, bcs=None, diagonal: float = 1.0, A: MatrixCSR | None = None, method: str = "gather") -> MatrixCSR:
+def assemble_matrix(a, bcs=None, diagonal: float = 1.0, A: MatrixCSR | None = None, method: str = "gather",
+                    deterministic: bool = False, plan: dict | None = None, check: bool = False) -> MatrixCSR:
     """Assemble the bilinear form into a BSR matrix (dolfinx.fem.assemble_matrix + set_diagonal).
 
     bcs: list of DirichletBC — their rows and columns receive no cell contribution and their
     diagonal entries are set to `diagonal`. method: "gather" (row-gather, default) or
     "scatter" (element scatter with FP64 atomics; zeroes A first like MatZeroEntries).
+    deterministic: bit-identical values run to run (FA_DETERMINISTIC: exact 64-bit fixed-point
+    sums in the gather; affine-simplex linear elasticity with one Poisson ratio).
+    plan: gather_plan options (owner, slots, order, locality). check: synchronise and raise if a
+    kernel found a pattern entry missing (FA_CHECK_ERRORS).
     """
     V = a.V
     if A is None:
@@ -667,14 +675,19 @@ def assemble_matrix(a, bcs=None, diagonal: float = 1.0, A: MatrixCSR | None = No
         fb = _fa_bsr(A, part)
         if method == "gather":
             adj = V._fa_adjacency()
-            plan = gather_plan(V, A, part, a.kind)
-            rc = L.fa_assemble_matrix(ctypes.byref(fm), ctypes.byref(ff), ctypes.byref(adj), ctypes.byref(plan),
-                                      _lib.ptr(marker), float(diagonal), ctypes.byref(fb), _lib.FA_GATHER, sh)
+            gp = gather_plan(V, A, part, a.kind, deterministic=deterministic, **(plan or {}))
+            flags = _lib.FA_GATHER | (_lib.FA_DETERMINISTIC if deterministic else 0) | \
+                (_lib.FA_CHECK_ERRORS if check else 0)
+            rc = L.fa_assemble_matrix(ctypes.byref(fm), ctypes.byref(ff), ctypes.byref(adj), ctypes.byref(gp),
+                                      _lib.ptr(marker), float(diagonal), ctypes.byref(fb), flags, sh)
         elif method == "scatter":
+            flags = _lib.FA_SCATTER | _lib.FA_ZERO_FIRST | (_lib.FA_CHECK_ERRORS if check else 0)
             rc = L.fa_assemble_matrix(ctypes.byref(fm), ctypes.byref(ff), None, None, _lib.ptr(marker),
-                                      float(diagonal), ctypes.byref(fb), _lib.FA_SCATTER | _lib.FA_ZERO_FIRST, sh)
+                                      float(diagonal), ctypes.byref(fb), flags, sh)
         else:
             raise ValueError(f"unknown method {method}")
+        if deterministic and method != "gather":
+            raise ValueError("deterministic assembly is a gather mode")
         _lib.check(rc, "fa_assemble_matrix")
     A._keepalive = (marker, a)
     return A
@@ -687,8 +700,11 @@ class SplitGather:
     part must be in exactly one range for a complete assembly. femasm.parallel uses it to start
     the interface exchange of a rank's slab while its interior rows assemble."""
 
-    def __init__(self, a, bcs, A: MatrixCSR, ranges, part: int = 0, diagonal: float = 1.0):
+    def __init__(self, a, bcs, A: MatrixCSR, ranges, part: int = 0, diagonal: float = 1.0,
+                 deterministic: bool = False, slots: bool = True, order: str = "positional"):
         V = a.V
+        if a.kind == _lib.FA_NEO_HOOKEAN and not (slots and order == "positional"):
+            raise ValueError("the neo-Hookean gather needs positional plans (slots=True, order='positional')")
         L = _lib.load()
         self.L, self.a, self.A, self.diagonal = L, a, A, float(diagonal)
         self.marker, _ = _combine_bcs(V, bcs, with_g=False)
@@ -703,9 +719,10 @@ class SplitGather:
         base = int(A.indptr[pr0])
         bs2 = A.bs * A.bs
         self.slots = None
-        if os.environ.get("FEMASM_SLOTS", "auto") in ("1", "auto"):
+        if slots:
             self.slots = torch.empty(V.mesh.num_cells * V.nn * V.nn, dtype=torch.int16, device=dev)
         self.subs, self.plans, self._keep = [], [], []
+        self._xver = _coords_version(V.mesh)
         for r0, r1 in ranges:
             if not (pr0 <= r0 <= r1 <= pr1):
                 raise ValueError(f"row range [{r0}, {r1}) outside part [{pr0}, {pr1})")
@@ -718,6 +735,8 @@ class SplitGather:
                 _lib.check(L.fa_plan_gather_form(ctypes.byref(self.fm), int(a.kind), ctypes.byref(self.adj),
                                                  ctypes.byref(fb), rs.data_ptr(), ctypes.byref(plan), self.sh),
                            "fa_plan_gather_form")
+            if deterministic:
+                plan.cell_flags |= _lib.FA_PLAN_DETERMINISTIC
             self.subs.append(fb)
             self.plans.append(plan)
             self._keep.append(rs)
@@ -733,10 +752,21 @@ class SplitGather:
             for i in live:
                 self.plans[i].slots = self.slots.data_ptr()
                 self.plans[i].slot_order = 0
-                e = _plan_order(V, self.fm, self.adj, self.subs[i], self.plans[i], self.sh, self.eadj)
+                e = _plan_order(V, self.fm, self.adj, self.subs[i], self.plans[i], self.sh, self.eadj, order)
                 self.eadj = e if e is not None else self.eadj
 
     def prepare(self):
+        # the plans' FA_PLAN_AFFINE flags describe the coordinates they were planned on: vertices
+        # moved in place since then re-run the library's per-cell affinity check (as gather_plan does)
+        m = self.a.V.mesh
+        now = _coords_version(m)
+        if now != self._xver:
+            self.fm = self.a.V._fa_mesh()  # mesh.x may be a new tensor
+            if m.cell_type in (CellType.quadrilateral, CellType.hexahedron):
+                for plan in self.plans:
+                    _lib.check(self.L.fa_plan_check_affine(ctypes.byref(self.fm), ctypes.byref(plan), self.sh),
+                               "fa_plan_check_affine")
+            self._xver = now
         _lib.check(self.L.fa_gather_prepare(ctypes.byref(self.fm), ctypes.byref(self.ff), _lib.ptr(self.marker),
                                             self.work.data_ptr(), self.sh), "fa_gather_prepare")
 

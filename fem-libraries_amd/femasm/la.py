@@ -11,11 +11,10 @@ import numpy as np
 import torch
 
 
-# Largest single values allocation; larger matrices are split into row parts (each assembled
-# through the fa_bsr row window). Config E (138 GB) fits one part on a 288 GB MI355X.
-import os
-
-MAX_PART_BYTES = int(float(os.environ.get("FEMASM_MAX_PART_GB", "200")) * (1 << 30))
+# Largest single values allocation by default (create_matrix(max_part_bytes=...) sets another);
+# larger matrices are split into row parts (each assembled through the fa_bsr row window).
+# Config E (138 GB) fits one part on a 288 GB MI355X.
+MAX_PART_BYTES = 200 * (1 << 30)
 
 
 class MatrixCSR:

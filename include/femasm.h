@@ -63,6 +63,18 @@ extern "C" {
 #define FA_GATHER 0x0        /* row-gather: each BSR row computed once, plain coalesced stores */
 #define FA_SCATTER 0x1       /* element-scatter with FP64 atomics (dolfinx/PETSc ADD_VALUES shape) */
 #define FA_ZERO_FIRST 0x2    /* FA_SCATTER only: zero A->data first (MatZeroEntries) */
+#define FA_DETERMINISTIC 0x4 /* FA_GATHER: bit-reproducible values, run to run (see below) */
+#define FA_CHECK_ERRORS 0x8  /* synchronise `stream` and return FA_E_PATTERN if a kernel found a (row, column)
+                                pair or a Dirichlet diagonal missing from the pattern (debugging) */
+/* Deterministic assembly (FA_DETERMINISTIC, or FA_PLAN_DETERMINISTIC in plan->cell_flags, which
+ * fa_gather_rows honours too): the row gather adds every element contribution v of a row chunk as
+ * the 64-bit integer round(v * 2^s) (s per chunk from a bound on its contributions, |v 2^s| < 2^50)
+ * with integer LDS atomics, so each block's sum is exact and the same in any order, then converts
+ * it back with one rounding: the values are identical run to run. Per value the result is within
+ * ~2^-50 of the chunk's largest contribution bound per summand of the exact sum. For affine-simplex
+ * linear elasticity with one Poisson ratio (the k_gather_lin kernels) and a positional plan; other
+ * forms return FA_E_UNSUPPORTED. (The reference's MFEM integrator is likewise order-fixed: it runs
+ * one thread, MFEM/mechanic2d/asym_elasto_damage_model.cc:27.) */
 
 typedef struct {
   int32_t cell_type;     /* FA_TRIANGLE ... */
@@ -113,6 +125,8 @@ typedef struct {
 #define FA_PLAN_AFFINE 0x1   /* every cell of a tensor mesh is a parallelogram / parallelepiped: its
                                 hexahedra assemble through the affine row gather (no element-matrix
                                 store); otherwise through the MFMA element kernel + block gather */
+#define FA_PLAN_DETERMINISTIC 0x2 /* set by the caller: assemblies with this plan (fa_assemble_matrix and
+                                     fa_gather_rows) are deterministic, as with FA_DETERMINISTIC */
 
 /* Row-chunk plan for the gather kernel (host-computed once per pattern). */
 typedef struct {
@@ -158,7 +172,8 @@ int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A
 /* fa_plan_gather for the kernel of a form kind: FA_NEO_HOOKEAN chunks fill a larger accumulator
  * and aim at 128 adjacency entries (one round of the workgroup's 256 item lanes); other kinds are
  * fa_plan_gather. fa_assemble_matrix refuses a plan whose chunks exceed the form kernel's
- * accumulator (FA_E_ARG). */
+ * accumulator (FA_E_ARG). Neo-Hookean forms assemble only with a positional plan (fa_plan_slots +
+ * fa_plan_order with an entry buffer). */
 int fa_plan_gather_form(const fa_mesh* mesh, int32_t kind, const fa_adjacency* adj, const fa_bsr* A,
                         int64_t* row_start, fa_plan* plan, void* stream);
 
@@ -231,8 +246,9 @@ int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, const fa_adjace
  * `bc` must be the same in both calls. Same semantics per row as fa_assemble_matrix; elements /
  * forms without a gather kernel return FA_E_UNSUPPORTED. Neo-Hookean simplex forms prepare the
  * records of the M gather (k_gather_neo), whose plans must be positional (fa_plan_gather_form +
- * fa_plan_slots + fa_plan_order with an entry buffer); fa_gather_rows refuses another plan with
- * FA_E_ARG unless the process sets FEMASM_NEO_M=0 (fa_assemble_matrix falls back by itself).
+ * fa_plan_slots + fa_plan_order with an entry buffer); another plan is refused with FA_E_ARG
+ * (by fa_assemble_matrix too). The library reads no environment variable: results and accepted
+ * arguments depend on the arguments only.
  * (Replaces the same dolfinx call, FEniCSx/mechanic2d/asym_elasto_damage_model.cc:852-857, as
  * fa_assemble_matrix.) */
 int fa_gather_work_bytes(const fa_mesh* mesh, const fa_form* form, int64_t* bytes);

@@ -59,3 +59,22 @@ def test_version_and_element_info():
     assert (nn.value, nq.value) == (64, 64)
     assert L.fa_element_info(-4, 5, -1, ctypes.byref(nn), ctypes.byref(nq)) == -2
     assert b"unsupported" in L.fa_last_error()
+
+
+def test_library_reads_no_environment():
+    """The product library's results and accepted arguments depend on its arguments only: its
+    source reads no environment variable and the built library names none of the former tuning
+    switches (FEMASM_*); measurement variants are built out of tree (tools/r4/variant.py)."""
+    from femasm import _lib
+
+    src = open(os.path.join(ROOT, "fem-libraries_amd", "csrc", "femasm.hip")).read()
+    assert "getenv" not in src and "FEMASM_" not in src
+    if os.path.exists(_lib.LIB_PATH):
+        assert b"FEMASM_" not in open(_lib.LIB_PATH, "rb").read()
+    # nor does the host package (FEMASM_LIB, the library path, aside)
+    pkg = os.path.join(ROOT, "fem-libraries_amd", "femasm")
+    for f in os.listdir(pkg):
+        if f.endswith(".py"):
+            txt = open(os.path.join(pkg, f)).read()
+            names = set(re.findall(r"FEMASM_[A-Z_]+", txt)) - {"FEMASM_LIB"}
+            assert not names and "os.environ" not in txt.replace('os.environ.get("FEMASM_LIB")', ""), f

@@ -18,16 +18,15 @@ def dev():
     return torch.device("cuda", 0)
 
 
-@pytest.mark.parametrize("contrib", ["0", "1"], ids=["lds-atomic", "block-owner"])
+@pytest.mark.parametrize("owner", [False, True], ids=["lds-atomic", "block-owner"])
 @pytest.mark.parametrize("n", [203])
-def test_config_e_p2_tet_full_size(oracle, dev, monkeypatch, n, contrib):
+def test_config_e_p2_tet_full_size(oracle, dev, n, owner):
     """Config E mesh (203^3 x 6 = 50.2 M P2 tets, 202 M dofs) with the reference bcs, through the
-    default LDS-atomic gather and through the block-owner gather (FEMASM_CONTRIB=1: ~4.9 M chunks
-    of the contribution plan at full size)."""
+    default LDS-atomic gather and through the block-owner gather (owner=True: ~4.9 M chunks of the
+    contribution plan at full size)."""
     from femasm import fem, mesh
     from femasm.materials import e_range
 
-    monkeypatch.setenv("FEMASM_CONTRIB", contrib)
 
     m = mesh.create_unit_cube(n, n, n, mesh.CellType.tetrahedron, device=dev)
     V = fem.functionspace(m, ("Lagrange", 2, (3,)))
@@ -39,7 +38,7 @@ def test_config_e_p2_tet_full_size(oracle, dev, monkeypatch, n, contrib):
     A = fem.create_matrix(a)
     assert A.num_block_rows == (2 * n + 1) ** 3
     assert int(A.indptr[-1]) == A.num_blocks and bool((A.indptr[1:] >= A.indptr[:-1]).all())
-    fem.assemble_matrix(a, bcs=bcs, A=A)
+    fem.assemble_matrix(a, bcs=bcs, A=A, plan=dict(owner=owner))
     torch.cuda.synchronize()
     marker, _ = fem._combine_bcs(V, bcs)
     rel, nrows = sampled_row_parity(oracle, V, a, A, marker, nsample=1500)

@@ -1,6 +1,6 @@
 """GPU: the uniform-nu affine-simplex gather (MAT_LINU: records s*Ji with s^2 = mu|J|, table
 B = (lam/mu) Ahat + Ahat^T) against the CPU oracle, next to the general lam/mu kernel it replaces
-for E-per-cell forms: forms given as lam/mu arrays, FEMASM_LINU=0, and cells with E < 0 (the
+for E-per-cell forms: forms given as lam/mu arrays, and cells with E < 0 (the
 record's sign path). Bar as test_gpu_parity: |A - A_oracle|_max <= 1e-12 |A_oracle|_max."""
 import numpy as np
 import pytest
@@ -48,9 +48,8 @@ def _run(dev, oracle, ct_name, p, n, E_fn, use_lame, nu=0.3):
 
 
 @pytest.mark.parametrize("ct,p,n", CASES)
-@pytest.mark.parametrize("linu", ["1", "0"])
-def test_uniform_nu_and_general_kernel(dev, oracle, monkeypatch, linu, ct, p, n):
-    monkeypatch.setenv("FEMASM_LINU", linu)
+def test_uniform_nu_kernel(dev, oracle, ct, p, n):
+    """E per cell with one nu: the uniform-nu kernels (the general lam / mu kernel: test_lame_arrays)."""
     _run(dev, oracle, ct, p, n, lambda nc: oracle.e_range()[np.arange(nc) % 200], use_lame=False)
 
 

@@ -108,15 +108,10 @@ def test_lifting_matches_oracle(oracle, dev, ct, p, n):
 
 
 @pytest.mark.parametrize("ct,p,n", [(3, 2, (4, 3)), (-4, 1, (2, 3, 2)), (-4, 2, (3, 2, 3))])
-@pytest.mark.parametrize("neo_m,slot_order", [("1", "pos"), ("0", "pos"), ("1", "0")])
-def test_neohookean_gather_paths(oracle, dev, monkeypatch, ct, p, n, neo_m, slot_order):
-    """Both neo-Hookean gathers against the oracle with Dirichlet rows: k_gather_neo (M records, the
-    default; FEMASM_NEO_M=1) and k_gather's items (FEMASM_NEO_M=0), and a plan without the positional
-    order (FEMASM_SLOT_ORDER=0), on which fa_assemble_matrix falls back to k_gather's items."""
+def test_neohookean_gather_with_bcs(oracle, dev, ct, p, n):
+    """The neo-Hookean gather (k_gather_neo, M records) against the oracle with Dirichlet rows."""
     from femasm import fem
 
-    monkeypatch.setenv("FEMASM_NEO_M", neo_m)
-    monkeypatch.setenv("FEMASM_SLOT_ORDER", slot_order)
     m, V, a = _setup(oracle, ct, p, n, dev)
     left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
     right = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.ones_like(x[0])))
@@ -128,3 +123,13 @@ def test_neohookean_gather_paths(oracle, dev, monkeypatch, ct, p, n, neo_m, slot
     ref = oracle.assemble_neohookean(ct, p, _np(V.dofmap), _np(m.cells), _np(m.x), lam, mu, _np(a.u), indptr, indices,
                                      bc=_np(marker))
     assert np.abs(_np(A.data) - ref).max() <= RTOL * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("order", ["steps", "none"])
+def test_neohookean_needs_positional_plan(oracle, dev, order):
+    """A plan without the positional order is refused (FA_E_ARG), never assembled another way."""
+    from femasm import _lib, fem
+
+    m, V, a = _setup(oracle, -4, 2, (2, 2, 2), dev)
+    with pytest.raises(_lib.FemasmError, match="positional plan"):
+        fem.assemble_matrix(a, plan=dict(order=order))

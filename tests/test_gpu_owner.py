@@ -1,5 +1,5 @@
 """GPU parity of the block-owner gather (k_gather_own, contribution plan fa_plan_contrib; the
-default for triangles, FEMASM_CONTRIB=1 forces it for tetrahedra too) against the CPU oracle, with
+default for triangles, gather_plan(owner=True) forces it for tetrahedra too) against the CPU oracle, with
 the per-row 1e-12 bar of tests/rowparity.py.
 
 Covers P1/P2 triangles and tetrahedra with and without the reference's Dirichlet sets
@@ -25,11 +25,11 @@ def dev():
 
 
 @pytest.fixture
-def contrib(monkeypatch):
-    monkeypatch.setenv("FEMASM_CONTRIB", "1")
+def contrib():
+    return dict(owner=True)
 
 
-def _assemble(oracle, dev, ct, p, n, bcs_on, **kw):
+def _assemble(oracle, dev, ct, p, n, bcs_on, owner=True, **kw):
     from femasm import _lib, fem
 
     m = _mesh(ct, n, dev, **kw)
@@ -40,8 +40,8 @@ def _assemble(oracle, dev, ct, p, n, bcs_on, **kw):
         left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
         right = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.ones_like(x[0])))
         bcs = [fem.dirichletbc(0.0, left, V), fem.dirichletbc([0.01] + [0.0] * (m.gdim - 1), right, V)]
-    A = fem.assemble_matrix(a, bcs=bcs)
-    plan = fem.gather_plan(V, A, 0, _lib.FA_LINEAR_ELASTICITY)
+    A = fem.assemble_matrix(a, bcs=bcs, plan=dict(owner=owner))
+    plan = fem.gather_plan(V, A, 0, _lib.FA_LINEAR_ELASTICITY, owner=owner)
     torch.cuda.synchronize()
     return V, a, bcs, A, plan
 
@@ -80,32 +80,28 @@ def test_owner_gather_inverted_cells(oracle, dev, contrib):
     E = _E_cells(oracle, m.num_cells, dev)
     E[::7] *= -1.0
     a = fem.form(fem.LinearElasticity(V, E=E, nu=0.3))
-    A = fem.assemble_matrix(a, bcs=[])
+    A = fem.assemble_matrix(a, bcs=[], plan=contrib)
     from femasm import _lib
 
-    assert fem.gather_plan(V, A, 0, _lib.FA_LINEAR_ELASTICITY).contrib
+    assert fem.gather_plan(V, A, 0, _lib.FA_LINEAR_ELASTICITY, **contrib).contrib
     _, _, ref = _oracle_matrix(oracle, V, a)
     assert_rows_close(A.data.cpu().numpy(), ref, A.indptr.cpu().numpy(), RTOL)
 
 
 @pytest.mark.parametrize("ct,p,n", [(-4, 2, (7, 6, 5)), (3, 1, (30, 20)), (3, 2, (12, 9))])
-def test_owner_equals_lds_atomic_gather(oracle, dev, monkeypatch, ct, p, n):
-    from femasm import fem
-
+def test_owner_equals_lds_atomic_gather(oracle, dev, ct, p, n):
     out = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("FEMASM_CONTRIB", flag)
-        V, a, bcs, A, plan = _assemble(oracle, dev, ct, p, n, True)
-        assert bool(plan.contrib) == (flag == "1")
-        out[flag] = (A.data.cpu().numpy(), A.indptr.cpu().numpy())
-    assert_rows_close(out["1"][0], out["0"][0], out["0"][1], 1e-13)
+    for owner in (True, False):
+        V, a, bcs, A, plan = _assemble(oracle, dev, ct, p, n, True, owner=owner)
+        assert bool(plan.contrib) == owner
+        out[owner] = (A.data.cpu().numpy(), A.indptr.cpu().numpy())
+    assert_rows_close(out[True][0], out[False][0], out[False][1], 1e-13)
 
 
-def test_contrib_plan_refuses_oversized_chunks(oracle, dev, monkeypatch):
-    """fa_plan_contrib checks the chunking: a k_gather plan (up to 512 entries per chunk; with
-    FEMASM_LIN_GATHER=0, as simplex plans otherwise stop at k_gather_lin's 256 items) is refused
-    with FA_E_CAPACITY rather than overrunning the kernel's cell staging."""
-    monkeypatch.setenv("FEMASM_LIN_GATHER", "0")
+def test_contrib_plan_refuses_oversized_chunks(oracle, dev):
+    """fa_plan_contrib checks the chunking: a plan whose chunks hold more than 256 adjacency entries
+    (two chunks of half the rows each) is refused with FA_E_CAPACITY rather than overrunning the
+    kernel's cell staging."""
     import ctypes
 
     from femasm import _lib, fem
@@ -121,6 +117,10 @@ def test_contrib_plan_refuses_oversized_chunks(oracle, dev, monkeypatch):
     sh = _lib.stream_handle(dev)
     _lib.check(L.fa_plan_gather(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), rs.data_ptr(),
                                 ctypes.byref(plan), sh), "fa_plan_gather")
+    n = V.num_nodes
+    rs[:3] = torch.tensor([0, n // 2, n], dtype=torch.int64, device=dev)
+    plan.nchunks = 2
+    plan.max_adj = int(V.adjacency()[0][n].item())
     assert plan.max_adj > 256
     buf = torch.empty(16, dtype=torch.uint8, device=dev)
     rc = L.fa_plan_contrib(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), buf.data_ptr(), 16,

@@ -53,15 +53,14 @@ def test_vertices_moved_after_first_assembly(oracle, dev, ct, p, n):
 
 
 @pytest.mark.parametrize("ct,p,n", [(-4, 2, (5, 4, 6)), (-4, 1, (7, 6, 5)), (3, 1, (13, 11)), (3, 2, (9, 8))])
-def test_lin_gather_equals_generic_gather(oracle, dev, monkeypatch, ct, p, n):
-    """k_gather_lin (default for uniform-nu affine simplices) and k_gather (FEMASM_LIN_GATHER=0) give
-    the same matrix, both equal to the oracle, with the reference bcs."""
+def test_lin_gather_equals_generic_gather(oracle, dev, ct, p, n):
+    """k_gather_lin (the default for uniform-nu affine simplices: positional plans) and k_gather
+    (a plan with the plain slot map, order="none") give the same matrix, both equal to the oracle,
+    with the reference bcs."""
     from femasm import fem, mesh
 
-    monkeypatch.setenv("FEMASM_CONTRIB", "0")  # triangles: not the block-owner gather
     out = []
-    for lin in ("1", "0"):
-        monkeypatch.setenv("FEMASM_LIN_GATHER", lin)
+    for order in ("positional", "none"):  # owner=False: triangles not through the block-owner gather
         m = mesh.create_unit_square(*n, cell_type=ct, device=dev) if len(n) == 2 else \
             mesh.create_unit_cube(*n, cell_type=ct, device=dev)
         V = fem.functionspace(m, ("Lagrange", p, (m.gdim,)))
@@ -70,7 +69,7 @@ def test_lin_gather_equals_generic_gather(oracle, dev, monkeypatch, ct, p, n):
         left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
         right = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.ones_like(x[0])))
         bcs = [fem.dirichletbc(0.0, left, V), fem.dirichletbc([0.01] + [0.0] * (m.gdim - 1), right, V)]
-        A = fem.assemble_matrix(a, bcs=bcs)
+        A = fem.assemble_matrix(a, bcs=bcs, plan=dict(owner=False, order=order))
         marker, _ = fem._combine_bcs(V, bcs)
         ref = _oracle_vals(oracle, V, a, marker)
         assert_rows_close(A.data.cpu().numpy(), ref, A.indptr.cpu().numpy(), RTOL)
