@@ -1268,6 +1268,12 @@ __device__ __forceinline__ uint32_t cell_bcmask(const MeshView& M, const int8_t*
   return m;
 }
 
+// The uniform-nu record's last word is +-1 (the sign of mu |J|) with, for cells of <= 32 dofs, the
+// cell's constrained-dof bits in its low 32 mantissa bits (k_cell_records_staged): its sign and its
+// mask, without a separate mask load per item.
+__device__ __forceinline__ double rec_sign(double w) { return copysign(1.0, w); }
+__device__ __forceinline__ uint32_t rec_mask(double w) { return (uint32_t)__double_as_longlong(w); }
+
 template <int GD, int NN, int NV, int NQ, int MAT>
 __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, const double* __restrict__ tab,
                                                       const int8_t* __restrict__ bc, double* __restrict__ rec,
@@ -1304,6 +1310,10 @@ __global__ __launch_bounds__(256) void k_cell_records_staged(MeshView M, FormVie
     const int64_t cc = valid ? c : M.ncells - 1;
     double r[R::SIZE];
     cell_record<GD, NN, NV, NQ, MAT>(M, F, tab, cc, r);
+    uint32_t m = 0u;
+    if (bcmask && valid) m = cell_bcmask<GD, NN>(M, bc, c);
+    if constexpr (MAT == MAT_LINU && NN * GD <= 32)  // the mask also rides in the sign word (rec_sign)
+      r[GD * GD] = __longlong_as_double(__double_as_longlong(r[GD * GD]) | (long long)m);
 #pragma unroll
     for (int k = 0; k < R::SIZE; ++k) sb[lane * R::SIZE + k] = r[k];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1316,7 +1326,7 @@ __global__ __launch_bounds__(256) void k_cell_records_staged(MeshView M, FormVie
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (bcmask && valid) bcmask[c] = cell_bcmask<GD, NN>(M, bc, c);
+    if (bcmask && valid) bcmask[c] = m;
   }
 }
 
@@ -1853,7 +1863,7 @@ __global__ __launch_bounds__(256, kGatherWaves) void k_gather(GatherArgs P) {
 #pragma unroll
             for (int k = 0; k < GD; ++k) K[i][k] = i == k ? G[i][k] + tr : G[i][k];
           if (negw) {
-            const double sg = r[BS2];
+            const double sg = rec_sign(r[BS2]);
 #pragma unroll
             for (int i = 0; i < GD; ++i)
 #pragma unroll
@@ -2152,33 +2162,31 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
   // workgroup streams its own distant range: tools/probe/hbm_probe.py), and the chunks
   // that share cells run on one XCD at the same time (their records stay in its L2).
   const int G = gridDim.x;  // a multiple of 8
-  const int64_t pos = (int64_t)(blockIdx.x % 8) * (G / 8) + blockIdx.x / 8;
-  const int64_t cnt = pos < P.nchunks ? (P.nchunks - pos + G - 1) / G : 0;  // this workgroup's chunks
+  // 32-bit chunk indices (the host checks nchunks < 2^31): fewer SGPRs in the loop
+  const int pos = (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8);
+  const int cnt = pos < (int)P.nchunks ? ((int)P.nchunks - pos + G - 1) / G : 0;  // this workgroup's chunks
   if (cnt == 0) return;  // the whole workgroup
   (void)per;
   for (int t = tid; t < NN * NN * BS2; t += NT) tab[t] = P.ahat[t];
   for (int t = tid; t < NP2; t += NT) acc2[t] = dv2{0.0, 0.0};
   if (tid < 2) s_fx[tid] = 0u;
 
-  const int64_t abase = sload(P.A.indptr, P.A.row_begin);
-  const int64_t nent = P.M.ncells * NN;
   const int32_t* __restrict__ eadj = P.eadj;
-  const uint32_t* __restrict__ mk = P.bcmask ? P.bcmask : zero32;
-  const uint32_t mkmul = P.bcmask ? 1u : 0u;
-  struct Desc { int64_t b0, b1, a0, a1; };
-  auto desc = [&](int64_t i) -> Desc {  // the workgroup's i-th chunk, clamped to its last: static loads
-    const int64_t c = pos + min(i, cnt - 1) * G;
-    const int64_t r0 = sload(P.row_start, c), r1 = sload(P.row_start, c + 1);
-    return Desc{sload(P.A.indptr, r0), sload(P.A.indptr, r1), sload(P.adj_ptr, r0), sload(P.adj_ptr, r1)};
+  const uint32_t mkmul = P.bcmask ? 1u : 0u;  // FUSE: "has bcs" (the node bits are read only then)
+  // a chunk: first block and adjacency entry, block and entry counts (< 2^31 each: fa_plan_gather's caps);
+  // 6 SGPRs, and up to five in flight
+  struct Desc { int64_t b0, a0; int32_t nb, na; };  // b0 relative to the window's first block
+  // the workgroup's i-th chunk, clamped to its last: static loads of the per-launch chunk arrays
+  // (chunk_b: first block relative to the window, chunk_a: first adjacency entry; lin_chunk_desc)
+  auto desc = [&](int i) -> Desc {
+    const int c = pos + min(i, cnt - 1) * G;
+    const uint64_t n = (uint64_t)sload(P.chunk_a, (int64_t)P.nchunks + 1 + c);  // block count | entry count << 32
+    return Desc{sload(P.chunk_b, c), sload(P.chunk_a, c), (int32_t)(uint32_t)n, (int32_t)(n >> 32)};
   };
   const int jit = tid / NSPLIT, part = tid % NSPLIT;
-  // entry id (cell * NN + local row node) of this lane's item, clamped to a valid entry
-  auto load_entry = [&](const Desc& d) -> int32_t {
-    const int na = (int)(d.a1 - d.a0);
-    int64_t e = d.a0 + min(jit, max(na - 1, 0));
-    e = min(max(e, (int64_t)0), nent - 1);
-    return eadj[e];
-  };
+  // entry id (cell * NN + local row node) of this lane's item, clamped to a valid entry (chunk_a
+  // holds each chunk's first entry clamped below the entry count)
+  auto load_entry = [&](const Desc& d) -> int32_t { return eadj[d.a0 + min(jit, max(d.na - 1, 0))]; };
   // FUSE (P1 simplices, fa_assemble_matrix): no records kernel; an item loads its cell's vertex
   // coordinates, E and node bc bits (the vertex ids one chunk earlier still) and forms the uniform-nu
   // record in registers at the start of its chunk: one pipeline stage more (entries three chunks
@@ -2189,7 +2197,7 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     double r[RL];
     double x[FUSE ? NV1 : 1][GD];
     double E;
-    uint32_t sl[NBG];
+    uint32_t sl[(NBG + 1) / 2];  // the item's slot words, two 16-bit words per register
     uint32_t mask;
   };
   struct Vid { int32_t v[NV1]; };
@@ -2221,13 +2229,12 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
         it.r[2 * k + 1] = v.y;
       }
     }
-    const int na = (int)(d.a1 - d.a0);
-    int64_t e = d.a0 + min(jit, max(na - 1, 0));
-    e = min(max(e, (int64_t)0), nent - 1);
+    const int64_t e = d.a0 + min(jit, max(d.na - 1, 0));
     const uint16_t* sp = P.slots + e * NN + part * NBG;
 #pragma unroll
-    for (int bb = 0; bb < NBG; ++bb) it.sl[bb] = sp[bb];
-    if constexpr (!FUSE) it.mask = mk[c * mkmul] * mkmul;
+    for (int t = 0; t < (NBG + 1) / 2; ++t)
+      it.sl[t] = (uint32_t)sp[2 * t] | (2 * t + 1 < NBG ? (uint32_t)sp[2 * t + 1 < NBG ? 2 * t + 1 : 0] << 16 : 0u);
+    if constexpr (!FUSE) it.mask = rec_mask(it.r[GD * GD]);  // 0 without bcs (nothing was or-ed in)
   };
   // FUSE: the record (s Ji, sign of mu |J|) of the item's cell from its vertices (cell_record's
   // MAT_LINU branch on registers)
@@ -2273,7 +2280,7 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     return max(max(a, b), max(c, dd));
   };
   auto post_bound = [&](const Item& it, const Desc& d, int slot) {
-    const uint32_t e = wave_max(bound_exp(it, jit < (int)(d.a1 - d.a0)));
+    const uint32_t e = wave_max(bound_exp(it, jit < d.na));
     if ((tid & 63) == 0) atomicMax(&s_fx[slot], e);
   };
 
@@ -2298,7 +2305,7 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     post_bound(cur, d0, 0);
     __syncthreads();
   }
-  for (int64_t k = 0; k < cnt; ++k) {
+  for (int k = 0; k < cnt; ++k) {
     // L1: chunk k+2's entry ids; L2: chunk k+1's records / slots / masks (before chunk k's stores)
     // (FUSE: entries of chunk k+3, vertex ids of chunk k+2, coordinates of chunk k+1)
     int32_t pfn;
@@ -2319,10 +2326,10 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
       S = pow2(se);
     }
     // items of chunk k
-    const int64_t off = (d0.b0 - abase) * BS2;
+    const int64_t off = d0.b0 * BS2;
     const int h = (int)(off & 1);
-    const int nb = (int)(d0.b1 - d0.b0);
-    const bool valid = jit < (int)(d0.a1 - d0.a0);
+    const int nb = d0.nb;
+    const bool valid = jit < d0.na;
     {
       const int aloc = pf0 % NN;
       // single ds_read_b64 per value (volatile: not merged into ds_read2_b64, which costs 8 LDS
@@ -2348,14 +2355,15 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
       }
       double Bn[BS2];
       if constexpr (!P1G) {
-        const int b = (int)(cur.sl[0] >> 10);
+        const int b = (int)((cur.sl[0] >> 10) & 63u);
 #pragma unroll
         for (int e = 0; e < BS2; ++e) Bn[e] = Ah0[b * BS2 + e];
       }
 #pragma unroll
       for (int bb = 0; bb < NBG; ++bb) {
-        const int s = (int)(cur.sl[bb] & 1023u);
-        const int b = (int)(cur.sl[bb] >> 10);
+        const uint32_t slv = (cur.sl[bb / 2] >> (16 * (bb % 2))) & 0xFFFFu;
+        const int s = (int)(slv & 1023u);
+        const int b = (int)(slv >> 10);
         double G[GD][GD];
         if constexpr (P1G) {
           constexpr double cv = GD == 2 ? 0.5 : 1.0 / 6.0;  // reference simplex volume
@@ -2380,7 +2388,7 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
 #pragma unroll
         for (int e = 0; e < BS2; ++e) B[e] = Bn[e];
         if (bb + 1 < NBG) {  // next block's table entry: issued before this block's atomics
-          const int b1 = (int)(cur.sl[bb + 1 < NBG ? bb + 1 : bb] >> 10);
+          const int b1 = (int)((cur.sl[(bb + 1) / 2] >> (16 * ((bb + 1) % 2) + 10)) & 63u);
 #pragma unroll
           for (int e = 0; e < BS2; ++e) Bn[e] = Ah0[b1 * BS2 + e];
         }
@@ -2411,7 +2419,7 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
         for (int i = 0; i < GD; ++i) G[i][i] += tr;
         }
         if (negw) {
-          const double sg = cur.r[BS2];
+          const double sg = rec_sign(cur.r[BS2]);
 #pragma unroll
           for (int i = 0; i < GD; ++i)
 #pragma unroll
@@ -2469,6 +2477,24 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
       hv = tod(hv);
       tv = tod(tv);
     }
+    // stores: SW pair stores + the head and the tail value on every lane (a static count: see above),
+    // as buffer stores over the chunk's values; a lane without a pair (or the head / tail value)
+    // stores at an offset past the range, which the range check drops (no memory traffic)
+    {
+      typedef int v4i __attribute__((ext_vector_type(4)));
+      typedef unsigned v2u __attribute__((ext_vector_type(2)));
+      constexpr int OOB = 0x40000000, NTS = 2;  // nt
+      // one descriptor over the chunk's nv values; pair t at value h + 2t (16-B aligned)
+      const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(P.A.data + off, 0, 8 * nv, 0x00020000);
+      const int base = 8 * h + 16 * tid, lim = np - tid;  // pair tid + NT u: byte base + 16 NT u
+#pragma unroll
+      for (int u = 0; u < SW; ++u)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v[u]), rv, NT * u < lim ? base : OOB, 16 * NT * u,
+                                               NTS);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, hv), rv, (tid == 0 && h) ? 0 : OOB, 0, NTS);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rv,
+                                            (tid == 1 && ((nv - h) & 1)) ? 8 * (nv - 1) : OOB, 0, NTS);
+    }
     __syncthreads();  // B2: every read is done before any zero
 #pragma unroll
     for (int u = 0; u < SW; ++u)
@@ -2476,16 +2502,6 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     // the unpaired head (acc[1] when h = 1) and tail sit in pairs whose other half is never written
     if (tid == 0) acc2[0] = dv2{0.0, 0.0};
     if (tid == 1) acc2[(max(nv - 1, 0) + h) >> 1] = dv2{0.0, 0.0};
-    // stores: SW pair stores + the head and the tail value, on every lane (repeats write the same
-    // value to the same address)
-    // a chunk without values (rows of no cell) stores its repeats into a scratch line instead
-    const bool none = np < 1;
-    double* out = none ? dump : P.A.data + off;
-    dv2* out2 = reinterpret_cast<dv2*>(none ? dump : out + h);
-#pragma unroll
-    for (int u = 0; u < SW; ++u) lin_store(v[u], out2 + max(min(tid + NT * u, np - 1), 0));
-    lin_store(hv, out);
-    lin_store(tv, out + max(nv - 1, 0));
     if constexpr (FIX) {  // chunk k+1's scale from its prefetched items (records formed here for FUSE)
       form_record(nxt);
       post_bound(nxt, d1, (int)((k + 1) & 1));
@@ -3026,7 +3042,7 @@ __global__ __launch_bounds__(256, 3) void k_gather_own(GatherArgs P) {
               for (int kk = 1; kk < GD; ++kk) t = fma(Ah[i * GD + kk], r[kk * GD + d], t);
               T[i][d] = t;
             }
-          const double sg = valid ? r[BS2] : 0.0;  // sign of mu |J|; 0 drops a padding word
+          const double sg = valid ? rec_sign(r[BS2]) : 0.0;  // sign of mu |J|; 0 drops a padding word
           if (__any(sg != 1.0)) {                  // rare: an inverted cell or padding in the wave
 #pragma unroll
             for (int i = 0; i < GD; ++i)
@@ -4166,6 +4182,35 @@ static int chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
   return FA_OK;
 }
 
+// k_gather_lin's chunk arrays: per chunk c, chunk_b[c] = its first block relative to the window,
+// chunk_a[c] = its first adjacency entry (clamped below the entry count, so a lane's entry load is
+// always in range) and chunk_a[nchunks + 1 + c] = block count | entry count << 32: three scalar
+// loads per chunk, no dependent level, and fewer pointers live in the kernel's loop
+__global__ void k_lin_chunk_desc(const int64_t* __restrict__ row_start, int64_t nchunks, const int64_t* __restrict__ indptr,
+                                 int64_t row_begin, const int64_t* __restrict__ adj_ptr, int64_t nent,
+                                 int64_t* __restrict__ cb, int64_t* __restrict__ ca) {
+  const int64_t base = indptr[row_begin];
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r0 = row_start[c], r1 = row_start[c + 1];
+    const int64_t b0 = indptr[r0], a0 = adj_ptr[r0];
+    cb[c] = b0 - base;
+    ca[c] = min(a0, max(nent - 1, (int64_t)0));
+    ca[nchunks + 1 + c] = (int64_t)((uint64_t)(uint32_t)(indptr[r1] - b0) | ((uint64_t)(uint32_t)(adj_ptr[r1] - a0) << 32));
+  }
+}
+
+static int lin_chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
+  int rc;
+  if (P.nchunks >= (1ll << 31)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks (>= 2^31)", (long long)P.nchunks);
+  if ((rc = scratch_alloc((void**)buf, sizeof(int64_t) * 3 * (P.nchunks + 1), s))) return rc;
+  P.chunk_b = *buf;
+  P.chunk_a = *buf + (P.nchunks + 1);
+  k_lin_chunk_desc<<<grid_for(P.nchunks), 256, 0, s>>>(P.row_start, P.nchunks, P.A.indptr, P.A.row_begin, P.adj_ptr,
+                                                       P.M.ncells * P.M.nn, *buf, *buf + (P.nchunks + 1));
+  LAUNCH_CHECK();
+  return FA_OK;
+}
+
 // Gather grid. Default (dynamic): a persistent grid of the resident workgroup count (CUs x
 // occupancy, a multiple of 8 for the XCD order), each workgroup pulling chunks from its XCD's
 // counter with three chunks of look-ahead, so chunk k's stores, chunk k+1's metadata loads and
@@ -4361,6 +4406,8 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       if ((rc = lin_scratch(&zero32, &dump))) return rc;
       if (!nm) P.nodemask = reinterpret_cast<const uint8_t*>(zero32);  // a valid address (mask scaled by 0)
       P.fixc = lin_fix_bound(GD, NN, P.rlm, P.trc, P.amax);
+      int64_t* ldesc = nullptr;
+      if ((rc = lin_chunk_desc(P, &ldesc, s))) return rc;
       if (P.fix) {
         const int64_t grid = lin_grid(k_gather_lin<GD, NN, NSPLIT, LNT, true, true>, P.nchunks, LNT);
         k_gather_lin<GD, NN, NSPLIT, LNT, true, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
@@ -4369,6 +4416,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
         k_gather_lin<GD, NN, NSPLIT, LNT, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
       }
       LAUNCH_CHECK();
+      HIP_TRY(hipFreeAsync(ldesc, s));
       if (bc) {
         k_bc_diag<GD><<<grid_for((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
         LAUNCH_CHECK();
@@ -4422,6 +4470,8 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       double* dump = nullptr;
       if ((rc = lin_scratch(&zero32, &dump))) return rc;
       P.fixc = lin_fix_bound(GD, NN, rr, P.trc, P.amax);
+      int64_t* ldesc = nullptr;
+      if ((rc = lin_chunk_desc(P, &ldesc, s))) return rc;
       if (P.fix) {
         const int64_t grid = lin_grid(k_gather_lin<GD, NN, NSPLIT, LNT, false, true>, P.nchunks, LNT);
         k_gather_lin<GD, NN, NSPLIT, LNT, false, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
@@ -4430,6 +4480,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
         k_gather_lin<GD, NN, NSPLIT, LNT><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
       }
       LAUNCH_CHECK();
+      HIP_TRY(hipFreeAsync(ldesc, s));
       if (bc) {  // Dirichlet diagonals (dolfinx set_diagonal) of the plan's rows
         k_bc_diag<GD><<<grid_for((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
         LAUNCH_CHECK();

@@ -23,11 +23,11 @@ V = {
         "                if (q == 0x123456789ull) ap[i * GD + kk] = 1.0;"), (
         "              for (int kk = 0; kk < GD; ++kk) atomicAdd(ap + i * GD + kk, G[i][kk]);",
         "              for (int kk = 0; kk < GD; ++kk) if (G[i][kk] == 1.2345e-300) ap[i * GD + kk] = 1.0;")],
-    # no chunk stores to HBM
+    # no chunk stores to HBM (every store offset past the range)
     "lin_nostore": [(
-        "#pragma unroll\n    for (int u = 0; u < SW; ++u) lin_store(v[u], out2 + max(min(tid + NT * u, np - 1), 0));\n"
-        "    lin_store(hv, out);\n    lin_store(tv, out + max(nv - 1, 0));",
-        "    if (hv == 1.2345e-300) out[0] = tv + v[0].x + v[SW - 1].y;")],
+        "NT * u < lim ? base : OOB, 16 * NT * u,", "OOB, 16 * NT * u,"), (
+        "(tid == 0 && h) ? 0 : OOB, 0, NTS);", "OOB, 0, NTS);"), (
+        "(tid == 1 && ((nv - h) & 1)) ? 8 * (nv - 1) : OOB, 0, NTS);", "OOB, 0, NTS);")],
     # no accumulator zeroing in the drain
     "lin_nozero": [(
         "    for (int u = 0; u < SW; ++u)\n      if (tid + NT * u < np) acc2[h + tid + NT * u] = dv2{0.0, 0.0};",
