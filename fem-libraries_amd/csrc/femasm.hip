@@ -160,6 +160,35 @@ extern "C" int fa_element_info(int32_t cell_type, int32_t degree, int32_t qdeg, 
   return FA_OK;
 }
 
+typedef double fa_dv2 __attribute__((ext_vector_type(2)));
+// Store-data registers: a VALU write to a VGPR that a buffer_store_dwordx4 issued a few instructions
+// earlier still reads corrupts the stored value on gfx950 (measured: the low dword of a drained value
+// replaced by the next store's offset, 2 wait states after the store; the compiler inserts none or
+// two). The drains therefore keep their store data live until after the next barrier.
+// Outside the gathers' loops: wait for the wave's stores (their data has then been read), the
+// stored values kept live until then.
+__device__ __forceinline__ void store_fence() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
+template <int N>
+__device__ __forceinline__ void store_fence(const double (&v)[N]) {
+  store_fence();
+#pragma unroll
+  for (int u = 0; u < N; ++u) asm volatile("" ::"v"(v[u]));
+}
+template <int N, int M>
+__device__ __forceinline__ void store_fence(const double (&v)[N][M]) {
+  store_fence();
+#pragma unroll
+  for (int u = 0; u < N; ++u)
+#pragma unroll
+    for (int w = 0; w < M; ++w) asm volatile("" ::"v"(v[u][w]));
+}
+template <int N>
+__device__ __forceinline__ void keep_vgprs(const fa_dv2 (&v)[N], double a, double b) {
+#pragma unroll
+  for (int u = 0; u < N; ++u) asm volatile("" ::"v"(v[u]));
+  asm volatile("" ::"v"(a), "v"(b));
+}
+
 // AMD dispatches are limited to < 2^32 work-items (a larger grid fails silently): every kernel is
 // grid-stride and grids are capped at kMaxBlocks (x 256 threads < 2^32; multiple of 8 for the
 // XCD-aware gather order).
@@ -794,6 +823,7 @@ __global__ __launch_bounds__(256) void k_cell_blocks(MeshView M, FormView F, Dev
       for (int i = 0; i < GD; ++i)
 #pragma unroll
         for (int j = 0; j < GD; ++j) out[(a * GD + i) * nd + b * GD + j] = K[i][j];
+      store_fence(K);
     } else {
       int64_t na = M.cells[c * nn + a], nb = M.cells[c * nn + b];
       if (na < A.row_begin || na >= A.row_end) continue;
@@ -997,6 +1027,7 @@ __global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
           for (int i = 0; i < 3; ++i)
 #pragma unroll
             for (int k = 0; k < 3; ++k) out[(a * 3 + i) * (3 * NN) + b * 3 + k] = K[i][k];
+          store_fence(K);
         } else if (MODE == 2) {  // block store for the row gather: Eb[c][a][b][3][3], bc rows/cols zeroed
           double* out = Ae + ((ci * NN + a) * NN + b) * 9;
           const int64_t na = cn[a], nb = cn[b];
@@ -1286,6 +1317,7 @@ __global__ __launch_bounds__(256) void k_cell_records(MeshView M, FormView F, co
   double2* out = reinterpret_cast<double2*>(rec + c * R::SIZE);
 #pragma unroll
   for (int k = 0; k < R::SIZE / 2; ++k) out[k] = make_double2(r[2 * k], r[2 * k + 1]);
+  store_fence(r);
   }
   if (bcmask) bcmask[c] = cell_bcmask<GD, NN>(M, bc, c);
   }
@@ -2091,9 +2123,7 @@ __device__ __forceinline__ void lin_store(const T& v, T* p) {
   __builtin_nontemporal_store(v, p);
 }
 
-// chunk drain of k_gather_neo without the read / zero barrier (chunk_drain); k_gather_lin keeps the
-// two-barrier read-all / zero-all drain (at its 128-VGPR cap chunk_drain's buffer descriptor and pair
-// registers spill uniform pointers whose reloads wait vmcnt(0) in the item loop)
+// chunk drain of k_gather_neo without the read / zero barrier (chunk_drain)
 // Stream a chunk's nv accumulated values acc[h, h + nv) to out[0, nv) and leave the accumulator
 // zero, after the items barrier. The values form 16-B pairs acc2[j], j < j1 = (h + nv + 1) / 2; pair
 // j lands at out - h + 2j, 16-B aligned (out - h is). A lane reads, zeroes and stores its own pairs
@@ -2101,12 +2131,13 @@ __device__ __forceinline__ void lin_store(const T& v, T* p) {
 // pairs at the ends (head half when h = 1, tail half when h + nv is odd) are stored as single
 // values by their owners. Every lane issues exactly SW + 2 stores (lanes without a pair or a half
 // store to the scratch line `dump`): a static vector-memory count (see k_gather_lin).
+// The stored values are left in v / hv / tv for the caller's keep_vgprs after its next barrier.
 template <int SW, int NT = 256>
-__device__ __forceinline__ void chunk_drain(double* acc, int h, int nv, double* out, double* dump, int tid) {
-  typedef double dv2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void chunk_drain(double* acc, int h, int nv, double* out, int tid, fa_dv2 (&v)[SW],
+                                            double& hv, double& tv) {
+  typedef fa_dv2 dv2;
   typedef int v4i __attribute__((ext_vector_type(4)));
   typedef unsigned v2u __attribute__((ext_vector_type(2)));
-  (void)dump;
   dv2* acc2 = reinterpret_cast<dv2*>(acc);
   const int j1 = (h + nv + 1) >> 1;
   const int jt = (h + nv - 1) >> 1;             // the pair holding the last value
@@ -2116,17 +2147,18 @@ __device__ __forceinline__ void chunk_drain(double* acc, int h, int nv, double* 
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out - h, 0, (h + nv) * 8, 0x00020000);
   constexpr int OOB = 0x40000000;
   constexpr int AUX = 2;  // nt
-  double hv = 0.0, tv = 0.0;
+  hv = 0.0;
+  tv = 0.0;
 #pragma unroll
   for (int u = 0; u < SW; ++u) {
     const int j = tid + NT * u;
     const int jj = max(min(j, j1 - 1), 0);
-    const dv2 v = acc2[jj];
+    v[u] = acc2[jj];
     if (j < j1) acc2[jj] = dv2{0.0, 0.0};
-    if (j == 0) hv = v.y;
-    if (j == jt) tv = v.x;
+    if (j == 0) hv = v[u].y;
+    if (j == jt) tv = v[u].x;
     const bool full = j < j1 && !(j == 0 && h) && !(j == jt && tail_half);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), rs, full ? 16 * j : OOB, 0, AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v[u]), rs, full ? 16 * j : OOB, 0, AUX);
   }
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, hv), rs, (tid == 0 && h) ? 8 : OOB, 0, AUX);
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rs,
@@ -2135,6 +2167,11 @@ __device__ __forceinline__ void chunk_drain(double* acc, int h, int nv, double* 
 constexpr int FA_LIN_FUSE = 1;  // P1 simplices (fa_assemble_matrix): records formed inside k_gather_lin
 // 2^e for a normal exponent (|e| <= 1022), from its bits (no FP64 op: uniform e stays scalar)
 __device__ __forceinline__ double pow2(int e) { return __hiloint2double((e + 1023) << 20, 0); }
+
+// k_gather_lin's chunk schedule: a persistent grid of the resident workgroups pulls chunks from 8
+// per-XCD counters, which deal the chunks in blocks of kLinCB (config E 38.3 vs 38.7 ms with ~32
+// chunks per workgroup in a static range; C 1.23 vs 1.27 ms; block sizes 1 / 4 / 64 within 0.5 %)
+constexpr int kLinCB = 16;
 
 template <int GD, int NN, int NSPLIT, int NT = 256, bool FUSE = false, bool FIX = false>
 __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32_t* __restrict__ zero32,
@@ -2153,20 +2190,29 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
   __shared__ __attribute__((aligned(16))) double acc[2 * NP2];
   __shared__ double tab[NN * NN * BS2];
   __shared__ uint32_t s_fx[2];  // FIX: scale exponent of the chunks of each parity (max over their items)
+  constexpr int LOOK = FUSE ? 4 : 3;  // chunk descriptors in flight (d0 .. d[LOOK-1])
+  constexpr int AHEAD = LOOK + 2;     // chunk ids fetched ahead of the chunk being gathered
+  constexpr int RING = 8;
+  __shared__ int32_t s_id[RING];      // chunk id of iteration m at s_id[m % RING]
   dv2* acc2 = reinterpret_cast<dv2*>(acc);
   const int tid = threadIdx.x;
-  // Chunk schedule: rounds of G consecutive chunks; in each round the 8 XCDs take 8 adjacent blocks
-  // of G / 8 chunks (blocks b and b + 8 share an XCD under round-robin dispatch; speed only). The
-  // chunks being written at any time then lie in one window of ~G chunks (the HBM write stream
-  // measured 6.0-7.0 TB/s when concurrent writes are close together, 5.3-5.5 TB/s when every
-  // workgroup streams its own distant range: tools/probe/hbm_probe.py), and the chunks
-  // that share cells run on one XCD at the same time (their records stay in its L2).
-  const int G = gridDim.x;  // a multiple of 8
-  // 32-bit chunk indices (the host checks nchunks < 2^31): fewer SGPRs in the loop
-  const int pos = (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8);
-  const int cnt = pos < (int)P.nchunks ? ((int)P.nchunks - pos + G - 1) / G : 0;  // this workgroup's chunks
-  if (cnt == 0) return;  // the whole workgroup
+  // Chunk schedule (kLinCB): the chunks being written at any time lie in one window of the rows, and
+  // neighbouring chunks, which share cells, mostly run on one XCD (their records stay in its L2).
+  // 32-bit chunk indices (the host checks nchunks < 2^30): fewer SGPRs in the loop
+  const int xc = (int)(blockIdx.x % 8);  // the XCD under round-robin dispatch (speed only)
   (void)per;
+  // the j-th chunk of XCD counter x (blocks of kLinCB chunks dealt round-robin to the counters,
+  // so the 8 XCDs advance through the rows together and the chunks in flight stay close)
+  unsigned int* const lctr = reinterpret_cast<unsigned int*>(P.ctr) + 32 * xc;
+  auto chunk_of = [&](unsigned int j) -> int32_t {
+    return (int32_t)min((j / kLinCB * 8u + (unsigned)xc) * kLinCB + j % kLinCB, 0x7FFFFFFFu);
+  };
+  if (tid == 0) {
+    const unsigned int b = atomicAdd(lctr, (unsigned)AHEAD);
+#pragma unroll
+    for (int t = 0; t < AHEAD; ++t) s_id[t] = chunk_of(b + t);
+  }
+  __syncthreads();
   for (int t = tid; t < NN * NN * BS2; t += NT) tab[t] = P.ahat[t];
   for (int t = tid; t < NP2; t += NT) acc2[t] = dv2{0.0, 0.0};
   if (tid < 2) s_fx[tid] = 0u;
@@ -2178,10 +2224,13 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
   struct Desc { int64_t b0, a0; int32_t nb, na; };  // b0 relative to the window's first block
   // the workgroup's i-th chunk, clamped to its last: static loads of the per-launch chunk arrays
   // (chunk_b: first block relative to the window, chunk_a: first adjacency entry; lin_chunk_desc)
+  // (the chunk of ring slot i; past the last chunk a descriptor of no entries and nb = -1)
   auto desc = [&](int i) -> Desc {
-    const int c = pos + min(i, cnt - 1) * G;
+    const int raw = __builtin_amdgcn_readfirstlane(s_id[i % RING]);
+    const bool ok = raw < (int)P.nchunks;
+    const int c = ok ? raw : (int)P.nchunks - 1;
     const uint64_t n = (uint64_t)sload(P.chunk_a, (int64_t)P.nchunks + 1 + c);  // block count | entry count << 32
-    return Desc{sload(P.chunk_b, c), sload(P.chunk_a, c), (int32_t)(uint32_t)n, (int32_t)(n >> 32)};
+    return Desc{sload(P.chunk_b, c), sload(P.chunk_a, c), ok ? (int32_t)(uint32_t)n : -1, ok ? (int32_t)(n >> 32) : 0};
   };
   const int jit = tid / NSPLIT, part = tid % NSPLIT;
   // entry id (cell * NN + local row node) of this lane's item, clamped to a valid entry (chunk_a
@@ -2305,7 +2354,11 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     post_bound(cur, d0, 0);
     __syncthreads();
   }
-  for (int k = 0; k < cnt; ++k) {
+  for (int k = 0; d0.nb >= 0; ++k) {
+    // the id of chunk k + AHEAD
+    unsigned int rn = 0u;
+    // (atomicInc: the compiler's wave-aggregation of a uniform atomicAdd would wait for its return here)
+    if (tid == 0) rn = atomicInc(lctr, 0xFFFFFFFFu);
     // L1: chunk k+2's entry ids; L2: chunk k+1's records / slots / masks (before chunk k's stores)
     // (FUSE: entries of chunk k+3, vertex ids of chunk k+2, coordinates of chunk k+1)
     int32_t pfn;
@@ -2317,7 +2370,7 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
       pfn = load_entry(d2);
       load_item(d1, pf1, nxt, vid1);
     }
-    const Desc d4 = desc(k + (FUSE ? 4 : 3));
+    const Desc d4 = desc(k + LOOK);
     if constexpr (!FIX) form_record(cur);  // FIX: formed at the end of the previous chunk (its bound)
     int se = 0;
     double S = 1.0;
@@ -2458,14 +2511,30 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     }
     __syncthreads();  // B1: the chunk is accumulated
     if (FIX && tid == 0) s_fx[k & 1] = 0u;  // read by every item above; next written for chunk k + 2
-    // read the chunk into registers: pairs t (value 2t + h .. 2t + 1 + h at acc2[t + h]); lanes past
-    // the chunk's pairs repeat the last pair, and every lane reads the unpaired head / tail value
+    // read the chunk into registers and leave the accumulator zero: pairs t (value 2t + h .. 2t + 1 + h
+    // at acc2[t + h]) by lane t % NT, the unpaired head (acc[1] when h = 1) by lane 0, the unpaired
+    // tail by lane 1; no other lane touches them, so no barrier separates the reads from the zeroes
+    // (the other halves of the head / tail pairs are never written)
     const int nv = nb * BS2;
     const int np = (nv - h) >> 1;
+    const bool tail = ((nv - h) & 1) != 0;
     dv2 v[SW];
+    double hv = 0.0, tv = 0.0;
+    {  // ds_wrxchg_rtn_b64: 2 x 6.4 LDS clocks per 16 B against 4.1 + 13.0 for a 16-B read and zero write
+      auto xchg = [&](double* p) -> double {
+        return __hip_atomic_exchange(p, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      };
 #pragma unroll
-    for (int u = 0; u < SW; ++u) v[u] = acc2[h + max(min(tid + NT * u, np - 1), 0)];
-    double hv = acc[h], tv = acc[max(nv - 1, 0) + h];
+      for (int u = 0; u < SW; ++u) {
+        v[u] = dv2{0.0, 0.0};
+        if (tid + NT * u < np) {
+          double* pp = acc + 2 * (h + tid + NT * u);
+          v[u] = dv2{xchg(pp), xchg(pp + 1)};
+        }
+      }
+      if (tid == 0 && h) hv = xchg(acc + 1);
+      if (tid == 1 && tail) tv = xchg(acc + nv - 1 + h);
+    }
     if constexpr (FIX) {  // the integer sums back to doubles: (hi 2^32 + lo) 2^-se, one rounding
       const double c32 = pow2(32 - se), inv = pow2(-se);
       auto tod = [&](double x) -> double {
@@ -2492,21 +2561,17 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v[u]), rv, NT * u < lim ? base : OOB, 16 * NT * u,
                                                NTS);
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, hv), rv, (tid == 0 && h) ? 0 : OOB, 0, NTS);
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rv,
-                                            (tid == 1 && ((nv - h) & 1)) ? 8 * (nv - 1) : OOB, 0, NTS);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rv, (tid == 1 && tail) ? 8 * (nv - 1) : OOB, 0, NTS);
     }
-    __syncthreads();  // B2: every read is done before any zero
-#pragma unroll
-    for (int u = 0; u < SW; ++u)
-      if (tid + NT * u < np) acc2[h + tid + NT * u] = dv2{0.0, 0.0};
-    // the unpaired head (acc[1] when h = 1) and tail sit in pairs whose other half is never written
-    if (tid == 0) acc2[0] = dv2{0.0, 0.0};
-    if (tid == 1) acc2[(max(nv - 1, 0) + h) >> 1] = dv2{0.0, 0.0};
     if constexpr (FIX) {  // chunk k+1's scale from its prefetched items (records formed here for FUSE)
       form_record(nxt);
       post_bound(nxt, d1, (int)((k + 1) & 1));
     }
     __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics
+    keep_vgprs(v, hv, tv);
+    // chunk k + AHEAD's id, read at iteration k + AHEAD - LOOK = k + 2 (after B1 of k + 1); written
+    // here, where the wait for it is the one for chunk k+1's item loads (issued after it)
+    if (tid == 0) s_id[(k + AHEAD) % RING] = chunk_of(rn);
     // rotate the pipeline
     d0 = d1;
     d1 = d2;
@@ -2875,8 +2940,11 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
     // issued before chunk k's stores (their wait at chunk k+1 does not include the stores)
     load_item(d1, pf1, cur);
     __syncthreads();  // B1: the chunk is accumulated
-    chunk_drain<SW, NTH>(acc, h, nb * BS2, P.A.data + off, dump, tid);
+    fa_dv2 dv[SW];
+    double dh, dt;
+    chunk_drain<SW, NTH>(acc, h, nb * BS2, P.A.data + off, tid, dv, dh, dt);
     __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics
+    keep_vgprs(dv, dh, dt);
     d0 = d1;
     d1 = d2;
     d2 = d3;
@@ -4151,17 +4219,12 @@ __global__ void k_chunk_desc(const int64_t* __restrict__ row_start, int64_t nchu
   }
 }
 
-// k_gather_lin's grid: about FA_LIN_CHUNKS_PER_WG chunks per workgroup, never fewer workgroups than
-// are resident. A grid many times the resident count lets the dispatcher balance the chunks' uneven
-// cost across CUs and XCDs: config E 44.5 ms at the resident count (~4,700 chunks per workgroup),
-// 43.7 / 42.8 / 41.7 / 40.3 / 39.5 ms at 2 / 4 / 8 / 32 / 128 times it, 44.6 ms at 1024 times (~5 per
-// workgroup); config C (162 k chunks) best at 4-8 times (1.30 vs 1.34 ms), 1.46 at 32 times.
-constexpr int kLinChunksPerWg = 32;
-// k_gather_neo likewise, at ~kNeoChunksPerWg (config E-neo, alternating on one box: 74.0-74.3 ms
-// at 64 times the resident count against 75.5-76.9 at 1 time)
+// k_gather_neo's grid: about kNeoChunksPerWg chunks per workgroup in a static range, never fewer
+// workgroups than are resident (config E-neo, alternating on one box: 74.0-74.3 ms at 64 times the
+// resident count against 75.5-76.9 at 1 time). k_gather_lin's dynamic schedule runs the resident grid.
 constexpr int kNeoChunksPerWg = 128;
 template <typename K>
-static int64_t lin_grid(K kernel, int64_t nchunks, int block, int per_wg = kLinChunksPerWg) {
+static int64_t neo_grid(K kernel, int64_t nchunks, int block, int per_wg = kNeoChunksPerWg) {
   const int64_t g0 = gather_grid(kernel, nchunks, block);
   const int64_t per = (nchunks + 7) / 8;
   const int64_t g = std::max<int64_t>(g0, nchunks / per_wg / 8 * 8);
@@ -4201,10 +4264,12 @@ __global__ void k_lin_chunk_desc(const int64_t* __restrict__ row_start, int64_t 
 
 static int lin_chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
   int rc;
-  if (P.nchunks >= (1ll << 31)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks (>= 2^31)", (long long)P.nchunks);
-  if ((rc = scratch_alloc((void**)buf, sizeof(int64_t) * 3 * (P.nchunks + 1), s))) return rc;
+  if (P.nchunks >= (1ll << 30)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks (>= 2^30)", (long long)P.nchunks);
+  if ((rc = scratch_alloc((void**)buf, sizeof(int64_t) * (3 * (P.nchunks + 1) + 128), s))) return rc;
   P.chunk_b = *buf;
   P.chunk_a = *buf + (P.nchunks + 1);
+  P.ctr = reinterpret_cast<unsigned long long*>(*buf + 3 * (P.nchunks + 1));  // 8 counters, 128 B apart
+  HIP_TRY(hipMemsetAsync(P.ctr, 0, 1024, s));
   k_lin_chunk_desc<<<grid_for(P.nchunks), 256, 0, s>>>(P.row_start, P.nchunks, P.A.indptr, P.A.row_begin, P.adj_ptr,
                                                        P.M.ncells * P.M.nn, *buf, *buf + (P.nchunks + 1));
   LAUNCH_CHECK();
@@ -4334,7 +4399,7 @@ static int launch_gather_neo(GatherArgs P, const int8_t* bc, hipStream_t s, cons
     uint32_t* zero32 = nullptr;
     double* dump = nullptr;
     if ((rc = lin_scratch(&zero32, &dump))) return rc;
-    const int64_t grid = lin_grid(k_gather_neo<GD, NN, NQ, NSPLIT>, P.nchunks, 256, kNeoChunksPerWg);
+    const int64_t grid = neo_grid(k_gather_neo<GD, NN, NQ, NSPLIT>, P.nchunks, 256);
     k_gather_neo<GD, NN, NQ, NSPLIT><<<(unsigned)grid, 256, 0, s>>>(P, zero32, dump);
     LAUNCH_CHECK();
     if (bc) {  // Dirichlet diagonals (dolfinx set_diagonal) of the plan's rows
@@ -4409,10 +4474,10 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       int64_t* ldesc = nullptr;
       if ((rc = lin_chunk_desc(P, &ldesc, s))) return rc;
       if (P.fix) {
-        const int64_t grid = lin_grid(k_gather_lin<GD, NN, NSPLIT, LNT, true, true>, P.nchunks, LNT);
+        const int64_t grid = gather_grid(k_gather_lin<GD, NN, NSPLIT, LNT, true, true>, P.nchunks, LNT);
         k_gather_lin<GD, NN, NSPLIT, LNT, true, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
       } else {
-        const int64_t grid = lin_grid(k_gather_lin<GD, NN, NSPLIT, LNT, true>, P.nchunks, LNT);
+        const int64_t grid = gather_grid(k_gather_lin<GD, NN, NSPLIT, LNT, true>, P.nchunks, LNT);
         k_gather_lin<GD, NN, NSPLIT, LNT, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
       }
       LAUNCH_CHECK();
@@ -4473,10 +4538,10 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       int64_t* ldesc = nullptr;
       if ((rc = lin_chunk_desc(P, &ldesc, s))) return rc;
       if (P.fix) {
-        const int64_t grid = lin_grid(k_gather_lin<GD, NN, NSPLIT, LNT, false, true>, P.nchunks, LNT);
+        const int64_t grid = gather_grid(k_gather_lin<GD, NN, NSPLIT, LNT, false, true>, P.nchunks, LNT);
         k_gather_lin<GD, NN, NSPLIT, LNT, false, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
       } else {
-        const int64_t grid = lin_grid(k_gather_lin<GD, NN, NSPLIT, LNT>, P.nchunks, LNT);
+        const int64_t grid = gather_grid(k_gather_lin<GD, NN, NSPLIT, LNT>, P.nchunks, LNT);
         k_gather_lin<GD, NN, NSPLIT, LNT><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
       }
       LAUNCH_CHECK();

@@ -27,11 +27,29 @@ V = {
     "lin_nostore": [(
         "NT * u < lim ? base : OOB, 16 * NT * u,", "OOB, 16 * NT * u,"), (
         "(tid == 0 && h) ? 0 : OOB, 0, NTS);", "OOB, 0, NTS);"), (
-        "(tid == 1 && ((nv - h) & 1)) ? 8 * (nv - 1) : OOB, 0, NTS);", "OOB, 0, NTS);")],
-    # no accumulator zeroing in the drain
-    "lin_nozero": [(
-        "    for (int u = 0; u < SW; ++u)\n      if (tid + NT * u < np) acc2[h + tid + NT * u] = dv2{0.0, 0.0};",
-        "    for (int u = 0; u < SW; ++u)\n      if (tid + NT * u < np && hv == 1.2345e-300) acc2[h + tid + NT * u] = dv2{0.0, 0.0};")],
+        "(tid == 1 && tail) ? 8 * (nv - 1) : OOB, 0, NTS);", "OOB, 0, NTS);")],
+    # per-phase clocks of k_gather_lin (s_memtime at the barriers, summed per wave in LDS, then over
+    # the launch into the scratch line `dump`; block 0 prints the running totals at each launch start)
+    "lin_timing": [(
+        "  __shared__ int32_t s_id[RING];      // chunk id of iteration m at s_id[m % RING]\n  dv2* acc2 = reinterpret_cast<dv2*>(acc);\n  const int tid = threadIdx.x;",
+        "  __shared__ int32_t s_id[RING];\n  dv2* acc2 = reinterpret_cast<dv2*>(acc);\n  const int tid = threadIdx.x;\n"
+        "  __shared__ unsigned long long s_tm[NT / 64][16];\n"
+        "  if (tid < NT / 4) s_tm[tid / 16][tid % 16] = 0ull;\n"
+        "  unsigned long long* const tmo = reinterpret_cast<unsigned long long*>(dump);\n"
+        "  if (blockIdx.x == 0 && tid == 0) printf(\"lin_timing %llu %llu %llu %llu %llu %llu %llu %llu %llu\\n\", tmo[0], tmo[1], tmo[2], tmo[3], tmo[4], tmo[5], tmo[6], tmo[7], tmo[8]);\n"
+        "  unsigned long long t_prev = __builtin_amdgcn_s_memtime(), r_prev = __builtin_amdgcn_s_memrealtime();\n"
+        "#define FA_T(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if ((tid & 63) == 0) atomicAdd(&s_tm[tid >> 6][i], t_ - t_prev); t_prev = t_; }\n"), (
+        "    // the id of chunk k + AHEAD\n",
+        "    FA_T(6);\n    { const unsigned long long r_ = __builtin_amdgcn_s_memrealtime(); if ((tid & 63) == 0) { atomicAdd(&s_tm[tid >> 6][7], 1ull); atomicAdd(&s_tm[tid >> 6][8], r_ - r_prev); } r_prev = r_; }\n    // the id of chunk k + AHEAD\n"), (
+        "    __syncthreads();  // B1: the chunk is accumulated\n    if (FIX && tid == 0) s_fx[k & 1] = 0u;",
+        "    FA_T(0);\n    __syncthreads();  // B1: the chunk is accumulated\n    FA_T(1);\n    if (FIX && tid == 0) s_fx[k & 1] = 0u;"), (
+        "    if constexpr (FIX) {  // chunk k+1's scale",
+        "    FA_T(2);\n    if constexpr (FIX) {  // chunk k+1's scale"), (
+        "    __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics\n    keep_vgprs(v, hv, tv);\n",
+        "    FA_T(4);\n    __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics\n    keep_vgprs(v, hv, tv);\n    FA_T(5);\n"), (
+        "    cur = nxt;\n  }\n  if (bad) atomicOr(P.err, 1);\n}",
+        "    cur = nxt;\n  }\n  if (bad) atomicOr(P.err, 1);\n  __syncthreads();\n"
+        "  if (tid < 9) { unsigned long long t = 0; for (int w = 0; w < NT / 64; ++w) t += s_tm[w][tid]; atomicAdd(tmo + tid, t); }\n}")],
     # no reference-tensor table reads (constants instead)
     "lin_notab": [(
         "          for (int e = 0; e < BS2; ++e) Bn[e] = Ah0[b1 * BS2 + e];",
@@ -58,6 +76,11 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["--list"]:
         print("\n".join(V))
         raise SystemExit(0)
+    src = open(SRC).read()
+    for n in sys.argv[1:]:  # every pattern checked before any build starts
+        for old, _ in V[n]:
+            if old not in src:
+                raise SystemExit(f"variant {n}: pattern not found:\n{old}")
     procs = [build(n) for n in sys.argv[1:]]
     rc = 0
     for p, path in procs:
