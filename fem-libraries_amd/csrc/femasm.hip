@@ -80,7 +80,45 @@ struct DevTables {
   const double* lat;   // tensor cells: node lattice code a0 + 8 a1 + 64 a2 per node (as doubles)
   int ndoubles;
   double amax;         // simplex: max |ahat| entry (bounds the blocks of the fixed-point gather)
+  // simplex: ahat = N / D with small integers N (exact rational integrals), each block's GD x GD
+  // integers packed in one 64-bit word (pk_word); NULL if the element's table does not pack
+  const uint64_t* pk;
+  double pk_scale;     // 1 / sqrt(D)
+  double pk_amax;      // max |N|
 };
+
+// Packed reference-tensor block: GD x GD signed fields, entries 0..PK0-1 in the low dword at
+// PKW-bit offsets, the rest in the high dword (no field straddles the dwords).
+constexpr int pk_width(int gd) { return gd == 3 ? 6 : 16; }
+constexpr int pk_low(int gd) { return gd == 3 ? 5 : 2; }
+static bool pack_ahat(int nn, int td, const std::vector<double>& ahat, std::vector<uint64_t>& pk, double& scale,
+                      double& nmax) {
+  if (td != 2 && td != 3) return false;
+  const int w = pk_width(td), lo = pk_low(td), lim = (1 << (w - 1)) - 1;
+  for (int D = 1; D <= 100000; ++D) {
+    bool ok = true;
+    nmax = 0.0;
+    for (double v : ahat) {
+      const double n = std::nearbyint(v * D);
+      if (std::fabs(v * D - n) > 1e-9 * std::max(1.0, std::fabs(n)) || std::fabs(n) > lim) {
+        ok = false;
+        break;
+      }
+      nmax = std::max(nmax, std::fabs(n));
+    }
+    if (!ok) continue;
+    pk.assign((size_t)nn * nn, 0ull);
+    for (int t = 0; t < nn * nn; ++t)
+      for (int e = 0; e < td * td; ++e) {
+        const int64_t n = (int64_t)std::nearbyint(ahat[(size_t)t * td * td + e] * D);
+        const uint64_t f = (uint64_t)n & ((1ull << w) - 1);
+        pk[t] |= e < lo ? f << (w * e) : f << (32 + w * (e - lo));
+      }
+    scale = 1.0 / std::sqrt((double)D);
+    return true;
+  }
+  return false;
+}
 
 static std::mutex g_tab_mu;
 static std::map<std::tuple<int, int, int, int>, DevTables> g_tabs;
@@ -109,6 +147,7 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
   // reference tensor of grad-grad products (affine simplices: G_ab = |J| Ji^T Ahat_ab Ji)
   const size_t off_ahat = h.size();
   double amax = 0.0;
+  std::vector<double> ah;
   if (is_simplex(ct)) {
     for (int a = 0; a < T.nn; ++a)
       for (int b = 0; b < T.nn; ++b)
@@ -118,8 +157,20 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
             for (int q = 0; q < T.nq; ++q)
               v += T.wq[q] * T.dphi[((size_t)q * T.nn + a) * T.td + i] * T.dphi[((size_t)q * T.nn + b) * T.td + j];
             h.push_back(v);
+            ah.push_back(v);
             amax = std::max(amax, std::fabs(v));
           }
+  }
+  std::vector<uint64_t> pk;
+  double pk_scale = 0.0, pk_amax = 0.0;
+  size_t off_pk = 0;
+  if (is_simplex(ct) && pack_ahat(T.nn, T.td, ah, pk, pk_scale, pk_amax)) {
+    off_pk = h.size();
+    for (uint64_t q : pk) {
+      double d;
+      std::memcpy(&d, &q, 8);
+      h.push_back(d);
+    }
   }
   // tensor cells: 1-D matrices of the affine fast path and the node lattice codes
   size_t off_t1d = 0, off_lat = 0;
@@ -147,6 +198,9 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
   D.lat = is_simplex(ct) ? nullptr : d + off_lat;
   D.ndoubles = (int)h.size();
   D.amax = amax;
+  D.pk = off_pk ? reinterpret_cast<const uint64_t*>(d + off_pk) : nullptr;
+  D.pk_scale = pk_scale;
+  D.pk_amax = pk_amax;
   g_tabs[key] = D;
   *out = D;
   return FA_OK;
@@ -1204,6 +1258,8 @@ struct GatherArgs {
   int fix;
   double fixc;
   double amax;  // max |ahat| entry of the element (DevTables::amax)
+  const uint64_t* pk;  // packed integer reference tensor (DevTables::pk) or NULL
+  double pks, pkmax;   // its 1 / sqrt(D) and max |N|
   // contribution plan (fa_plan_contrib, k_gather_own) or NULL
   const int64_t* cw;       // [nchunks + 1] offsets of the chunks' word sections (u16 units)
   const int32_t* ccells;   // [nchunks][FA_OWN_CCAP] the chunk's distinct cells (-1 padded)
@@ -2184,11 +2240,13 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
   constexpr int NP2 = (NACC + 1) / 2;        // 16-B pairs of the accumulator
   constexpr int SW = (MAXB * BS2 / 2 + NT - 1) / NT;  // pair stores per lane per chunk
   constexpr int RL = R::SIZE;
-  static_assert(NN % NSPLIT == 0 && NN * GD <= 32 && RL % 2 == 0 && NN <= 63, "k_gather_lin: affine simplices");
   constexpr bool P1G = NN == GD + 1;
+  static_assert(NN % NSPLIT == 0 && NN * GD <= 32 && RL % 2 == 0 && NN <= 63, "k_gather_lin: affine simplices");
   typedef double dv2 __attribute__((ext_vector_type(2)));
   __shared__ __attribute__((aligned(16))) double acc[2 * NP2];
-  __shared__ double tab[NN * NN * BS2];
+  // the reference tensor, one packed integer block per (a, b) (pk_ahat: Ahat_ab = N_ab / D; the item
+  // records are scaled by 1 / sqrt(D)); P1 simplices use none
+  __shared__ uint64_t tab[P1G ? 1 : NN * NN];
   __shared__ uint32_t s_fx[2];  // FIX: scale exponent of the chunks of each parity (max over their items)
   constexpr int LOOK = FUSE ? 4 : 3;  // chunk descriptors in flight (d0 .. d[LOOK-1])
   constexpr int AHEAD = LOOK + 2;     // chunk ids fetched ahead of the chunk being gathered
@@ -2213,7 +2271,8 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     for (int t = 0; t < AHEAD; ++t) s_id[t] = chunk_of(b + t);
   }
   __syncthreads();
-  for (int t = tid; t < NN * NN * BS2; t += NT) tab[t] = P.ahat[t];
+  if constexpr (!P1G)
+    for (int t = tid; t < NN * NN; t += NT) tab[t] = P.pk[t];
   for (int t = tid; t < NP2; t += NT) acc2[t] = dv2{0.0, 0.0};
   if (tid < 2) s_fx[tid] = 0u;
 
@@ -2286,8 +2345,12 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     if constexpr (!FUSE) it.mask = rec_mask(it.r[GD * GD]);  // 0 without bcs (nothing was or-ed in)
   };
   // FUSE: the record (s Ji, sign of mu |J|) of the item's cell from its vertices (cell_record's
-  // MAT_LINU branch on registers)
+  // MAT_LINU branch on registers); table blocks: s Ji scaled by 1 / sqrt(D) of the packed table
   auto form_record = [&](Item& it) {
+    if constexpr (!P1G) {
+#pragma unroll
+      for (int kk = 0; kk < BS2; ++kk) it.r[kk] *= P.pks;
+    }
     if constexpr (FUSE) {
       double J[GD][GD], Ji[GD][GD];
 #pragma unroll
@@ -2385,10 +2448,8 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
     const bool valid = jit < d0.na;
     {
       const int aloc = pf0 % NN;
-      // single ds_read_b64 per value (volatile: not merged into ds_read2_b64, which costs 8 LDS
-      // cycles per wave-instruction against 2 per ds_read_b64 for the same 16 bytes per lane)
-      typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
-      lds_vdouble* Ah0 = (lds_vdouble*)(tab + aloc * NN * BS2);
+      // the row's packed blocks: one ds_read_b64 per block (nine for a table of doubles)
+      const uint64_t* Ah0 = tab + aloc * NN;
       const uint32_t rowm = (cur.mask >> (aloc * GD)) & ((1u << GD) - 1);
       const bool negw = __any(cur.r[BS2] < 0.0);  // wave-uniform: a cell with mu |J| < 0
       // P1 simplices (P1G): the scaled physical gradients are the rows of s Ji (node k >= 1) and minus
@@ -2406,12 +2467,21 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
           for (int kk = 0; kk < GD; ++kk) gA[d] = aloc == kk + 1 ? cur.r[kk * GD + d] : gA[d];
         }
       }
-      double Bn[BS2];
-      if constexpr (!P1G) {
-        const int b = (int)((cur.sl[0] >> 10) & 63u);
+      // B_ab = r N_ab + N_ab^T (the integers of the packed block)
+      auto unpack = [&](uint64_t q, double (&B)[BS2]) {
+        constexpr int W = pk_width(GD), LO = pk_low(GD);
+        const uint32_t q0 = (uint32_t)q, q1 = (uint32_t)(q >> 32);
+        double N[BS2];
 #pragma unroll
-        for (int e = 0; e < BS2; ++e) Bn[e] = Ah0[b * BS2 + e];
-      }
+        for (int e = 0; e < BS2; ++e)
+          N[e] = (double)(int)(e < LO ? __builtin_amdgcn_sbfe((int)q0, W * e, W) : __builtin_amdgcn_sbfe((int)q1, W * (e - LO), W));  // sbfe is typed unsigned
+#pragma unroll
+        for (int i = 0; i < GD; ++i)
+#pragma unroll
+          for (int k = 0; k < GD; ++k) B[i * GD + k] = fma(P.rlm, N[i * GD + k], N[k * GD + i]);
+      };
+      uint64_t qn = 0ull;
+      if constexpr (!P1G) qn = Ah0[(cur.sl[0] >> 10) & 63u];
 #pragma unroll
       for (int bb = 0; bb < NBG; ++bb) {
         const uint32_t slv = (cur.sl[bb / 2] >> (16 * (bb % 2))) & 0xFFFFu;
@@ -2438,13 +2508,9 @@ __global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32
             for (int kk = 0; kk < GD; ++kk) G[i][kk] = fma(ra * gA[i], gB[kk], cv * gB[i] * gA[kk]) + (i == kk ? cv * dot : 0.0);
         } else {
         double B[BS2];
-#pragma unroll
-        for (int e = 0; e < BS2; ++e) B[e] = Bn[e];
-        if (bb + 1 < NBG) {  // next block's table entry: issued before this block's atomics
-          const int b1 = (int)((cur.sl[(bb + 1) / 2] >> (16 * ((bb + 1) % 2) + 10)) & 63u);
-#pragma unroll
-          for (int e = 0; e < BS2; ++e) Bn[e] = Ah0[b1 * BS2 + e];
-        }
+        unpack(qn, B);
+        if (bb + 1 < NBG)  // next block's table entry: issued before this block's atomics
+          qn = Ah0[(cur.sl[(bb + 1) / 2] >> (16 * ((bb + 1) % 2) + 10)) & 63u];
         // G = (s Ji)^T B (s Ji), column by column; K = G + tr(G) / (1 + r) I
 #pragma unroll
         for (int dd = 0; dd < GD; ++dd) {
@@ -4517,24 +4583,19 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   if constexpr (MAT == MAT_LINU && R::SIMP && NN % NSPLIT == 0 && NN * GD <= 32 && NN < 64) {
     // the store-decoupled gather (k_gather_lin): positional plans of <= 256 items per chunk
     constexpr int LNT = lin_threads(GD, NN);
-    if (P.nchunks > 0 && W.mode != GatherStage::PREP && !P.cw && P.eadj && P.slots &&
+    if (P.nchunks > 0 && W.mode != GatherStage::PREP && !P.cw && P.eadj && P.slots && (NN == GD + 1 || P.pk) &&
         P.slot_order == NSPLIT && !P.corder && P.plan_maxadj * NSPLIT <= LNT && P.plan_maxadj >= 0) {
       if (P.plan_maxb > gather_maxb(false, GD * GD))
         return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, the kernel %d", P.plan_maxb,
                     gather_maxb(false, GD * GD));
       if (P.nchunks >= (1ll << 31)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks", (long long)P.nchunks);
       const double nu = P.F.nu, rr = 2.0 * nu / (1.0 - 2.0 * nu);
-      double* bhat = nullptr;
-      if ((rc = scratch_alloc((void**)&bhat, sizeof(double) * NN * NN * GD * GD, s))) return rc;
-      k_bhat<GD><<<grid_for(NN * NN), 256, 0, s>>>(P.ahat, NN * NN, rr, bhat);
-      LAUNCH_CHECK();
-      P.ahat = bhat;
       P.trc = 1.0 / (1.0 + rr);
       P.rlm = rr;
       uint32_t* zero32 = nullptr;
       double* dump = nullptr;
       if ((rc = lin_scratch(&zero32, &dump))) return rc;
-      P.fixc = lin_fix_bound(GD, NN, rr, P.trc, P.amax);
+      P.fixc = lin_fix_bound(GD, NN, rr, P.trc, P.pkmax);  // records scaled by 1 / sqrt(D): |N| bounds
       int64_t* ldesc = nullptr;
       if ((rc = lin_chunk_desc(P, &ldesc, s))) return rc;
       if (P.fix) {
@@ -4550,7 +4611,6 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
         k_bc_diag<GD><<<grid_for((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
         LAUNCH_CHECK();
       }
-      HIP_TRY(hipFreeAsync(bhat, s));
       if (W.mode == GatherStage::FULL) {
         HIP_TRY(hipFreeAsync(rec, s));
         if (mask) HIP_TRY(hipFreeAsync(mask, s));
@@ -4780,6 +4840,7 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     P.t1d = T.t1d; P.lat = T.lat;
     P.fix = ((flags & FA_DETERMINISTIC) || (plan->cell_flags & FA_PLAN_DETERMINISTIC)) ? 1 : 0;
     P.amax = T.amax;
+    P.pk = T.pk; P.pks = T.pk_scale; P.pkmax = T.pk_amax;
     set_contrib(P, plan);
     if (P.fix && P.cw) return fail(FA_E_UNSUPPORTED, "deterministic assembly: not with a contribution plan");
     bool handled = false;
@@ -4860,6 +4921,7 @@ static int gather_stage(const fa_mesh* mesh, const fa_form* form, const fa_adjac
     P.eadj = P.slot_order ? plan->eadj : nullptr;
     P.fix = (plan->cell_flags & FA_PLAN_DETERMINISTIC) ? 1 : 0;
     P.amax = T.amax;
+    P.pk = T.pk; P.pks = T.pk_scale; P.pkmax = T.pk_amax;
     set_contrib(P, plan);
     if (P.fix && P.cw) return fail(FA_E_UNSUPPORTED, "deterministic assembly: not with a contribution plan");
   }
