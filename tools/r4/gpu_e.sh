@@ -12,7 +12,7 @@ L = [l.split()[1:] for l in open(sys.argv[1]) if l.startswith('lin_timing')]
 a, b = [list(map(int, x)) for x in L[-2:]]
 d = [y - x for x, y in zip(a, b)]
 n = d[7]
-names = ['items', 'B1', 'drain', '-', 'post', 'B3', 'bottom']
+names = ['items', 'B1', 'xchg', 'stores', 'post', 'B3', 'bottom']
 tot = sum(d[:7])
 print(sys.argv[2], 'wave-iterations', n, 'clocks/iter', ' '.join(f'{k}={v / n:.0f}' for k, v in zip(names, d)), 'total', f'{tot / n:.0f}', 'MHz', f'{100.0 * tot / max(d[8], 1):.0f}')
 js = [l for l in open(sys.argv[1]) if l.startswith('{')]

@@ -44,7 +44,9 @@ V = {
         "    __syncthreads();  // B1: the chunk is accumulated\n    if (FIX && tid == 0) s_fx[k & 1] = 0u;",
         "    FA_T(0);\n    __syncthreads();  // B1: the chunk is accumulated\n    FA_T(1);\n    if (FIX && tid == 0) s_fx[k & 1] = 0u;"), (
         "    if constexpr (FIX) {  // chunk k+1's scale",
-        "    FA_T(2);\n    if constexpr (FIX) {  // chunk k+1's scale"), (
+        "    FA_T(3);\n    if constexpr (FIX) {  // chunk k+1's scale"), (
+        "    if constexpr (FIX) {  // the integer sums back to doubles",
+        "    __builtin_amdgcn_s_waitcnt(0xC07F);\n    FA_T(2);\n    if constexpr (FIX) {  // the integer sums back to doubles"), (
         "    __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics\n    keep_vgprs(v, hv, tv);\n",
         "    FA_T(4);\n    __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics\n    keep_vgprs(v, hv, tv);\n    FA_T(5);\n"), (
         "    cur = nxt;\n  }\n  if (bad) atomicOr(P.err, 1);\n}",
