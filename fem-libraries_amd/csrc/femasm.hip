@@ -1185,6 +1185,13 @@ __host__ __device__ constexpr int gather_maxb(bool neo, int bs2) {
   return (neo ? kGatherLdsNeo : kGatherLdsValues) / (8 * bs2) < 1023 ? (neo ? kGatherLdsNeo : kGatherLdsValues) / (8 * bs2)
                                                                       : 1023;
 }
+// k_gather_lin for P1 simplices: chunks are entry-bound (config C: ~160 blocks), so a 16 KB
+// accumulator and more resident waves
+constexpr int kLinLdsP1 = 16384;
+constexpr int kLinWavesP1 = 4;
+__host__ __device__ constexpr int lin_maxb(int gd, int nn) {
+  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gather_maxb(false, gd * gd);
+}
 static constexpr int kGatherMaxAdj = 512;       // adjacency entries per chunk
 static constexpr int kGatherMaxRows = 128;      // rows per chunk
 
@@ -2230,12 +2237,12 @@ __device__ __forceinline__ double pow2(int e) { return __hiloint2double((e + 102
 constexpr int kLinCB = 16;
 
 template <int GD, int NN, int NSPLIT, int NT = 256, bool FUSE = false, bool FIX = false>
-__global__ __launch_bounds__(NT, 4) void k_gather_lin(GatherArgs P, const uint32_t* __restrict__ zero32,
+__global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_lin(GatherArgs P, const uint32_t* __restrict__ zero32,
                                                         double* __restrict__ dump, int64_t per) {
   using R = Rec<GD, GD + 1, 1, MAT_LINU>;
   constexpr int BS2 = GD * GD;
   constexpr int NBG = NN / NSPLIT;
-  constexpr int MAXB = gather_maxb(false, BS2);
+  constexpr int MAXB = lin_maxb(GD, NN);
   constexpr int NACC = MAXB * BS2 + 2;       // value p of a chunk at acc[p + h], h = its parity
   constexpr int NP2 = (NACC + 1) / 2;        // 16-B pairs of the accumulator
   constexpr int SW = (MAXB * BS2 / 2 + NT - 1) / NT;  // pair stores per lane per chunk
@@ -3876,7 +3883,10 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
     int rc = get_tables(mesh->cell_type, mesh->degree, -1, &T);
     if (rc) return rc;
     const int ns = lin_simplex_nsplit(mesh->cell_type, mesh->degree, T.nq);
-    if (ns > 0) maxadj = std::min(maxadj, lin_threads(mesh->gdim, mesh->nn) / ns);
+    if (ns > 0) {
+      maxadj = std::min(maxadj, lin_threads(mesh->gdim, mesh->nn) / ns);
+      return plan_gather(mesh, adj, A, row_start, plan, stream, lin_maxb(mesh->gdim, mesh->nn), maxadj);
+    }
   }
   return plan_gather(mesh, adj, A, row_start, plan, stream, gather_maxb(false, mesh->gdim * mesh->gdim), maxadj);
 }
@@ -4518,7 +4528,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     constexpr int LNT = lin_threads(GD, NN);
     if (W.mode == GatherStage::FULL && P.nchunks > 0 && P.F.E && !P.cw && P.eadj &&
         P.slots && P.slot_order == NSPLIT && !P.corder && P.plan_maxadj * NSPLIT <= LNT && P.plan_maxadj >= 0 &&
-        P.plan_maxb <= gather_maxb(false, GD * GD) && P.nchunks < (1ll << 31)) {
+        P.plan_maxb <= lin_maxb(GD, NN) && P.nchunks < (1ll << 31)) {
       int rc;
       uint8_t* nm = nullptr;
       if (bc) {
@@ -4585,9 +4595,8 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     constexpr int LNT = lin_threads(GD, NN);
     if (P.nchunks > 0 && W.mode != GatherStage::PREP && !P.cw && P.eadj && P.slots && (NN == GD + 1 || P.pk) &&
         P.slot_order == NSPLIT && !P.corder && P.plan_maxadj * NSPLIT <= LNT && P.plan_maxadj >= 0) {
-      if (P.plan_maxb > gather_maxb(false, GD * GD))
-        return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, the kernel %d", P.plan_maxb,
-                    gather_maxb(false, GD * GD));
+      if (P.plan_maxb > lin_maxb(GD, NN))
+        return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, the kernel %d", P.plan_maxb, lin_maxb(GD, NN));
       if (P.nchunks >= (1ll << 31)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks", (long long)P.nchunks);
       const double nu = P.F.nu, rr = 2.0 * nu / (1.0 - 2.0 * nu);
       P.trc = 1.0 / (1.0 + rr);
