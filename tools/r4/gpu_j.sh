@@ -4,7 +4,8 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 for c in ${CFGS:-E}; do
-for d in ${DETS:-""}; do
+for dm in ${DETS:-def}; do
+d=""; [ "$dm" = det ] && d="--deterministic"
 for name in ${VARS:-base}; do
   L=""; [ $name != base ] && L="FEMASM_LIB=$PWD/abl/libfemasm_$name.so"
   env $L timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-hbm-probe $d > gpurun_out/v.json 2> gpurun_out/v.err || { echo "$name failed"; tail -5 gpurun_out/v.err; exit 1; }
