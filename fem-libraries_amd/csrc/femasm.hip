@@ -3514,6 +3514,9 @@ extern "C" int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const
 // (chunk, quarter).
 // Positional plans (eperm != NULL): position jj of a chunk holds entry eperm[a0 + jj]; the plain
 // map is read from src and written by position, with chunk-relative block positions.
+// alternating-path moves of the slot order search (k_order_slots): rounds and lanes per chain
+constexpr int kKempeRounds = 4;
+constexpr int kKempeLen = 6;
 template <int NN, int NSPLIT>
 __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64_t* __restrict__ indptr,
                               const int64_t* __restrict__ adj_ptr, int64_t nchunks, int groups_per_chunk,
@@ -3613,6 +3616,56 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
       }
     };
     descend();
+    // Alternating-path (Kempe) moves between two steps, which the pairwise descent cannot make: a
+    // lane on a residue that two lanes hit at step t1 swaps its blocks of steps t1 and t2; the
+    // residue it brings to t1 may collide there with another lane, which swaps its t1 / t2 blocks
+    // too, and so on (at most kKempeLen lanes). A chain is kept when the two steps' passes drop,
+    // otherwise undone; then the descent runs again. (config E: passes 1.30 x the per-quarter bound
+    // max(steps, largest residue count) after the descent alone; tools/r4/plan_stats.py)
+    if constexpr (kKempeRounds > 0 && NBG > 1) {
+      auto res_at = [&](int q, int t) { return (int)res[q][pick[q][t]]; };
+      for (int round = 0; round < kKempeRounds; ++round) {
+        bool improved = false;
+        for (int t1 = 0; t1 < NBG; ++t1) {
+          for (int r = 0; r < 16; ++r) {
+            if (cnt[t1][r] < 2) continue;
+            int q0 = -1;
+            for (int q = 0; q < nl; ++q)
+              if (res_at(q, t1) == r) { q0 = q; break; }
+            bool done = false;
+            for (int t2 = 0; t2 < NBG && !done; ++t2) {
+              if (t2 == t1) continue;
+              const int before = mx[t1] + mx[t2];
+              int path[kKempeLen], len = 0;
+              int q = q0;
+              while (true) {
+                swap_pick(q, t1, t2);
+                path[len++] = q;
+                const int rn = res_at(q, t1);  // brought from t2
+                if (cnt[t1][rn] < 2 || len == kKempeLen) break;
+                int qn = -1;
+                for (int qq = 0; qq < nl && qn < 0; ++qq) {
+                  if (res_at(qq, t1) != rn) continue;
+                  bool used = false;
+                  for (int l = 0; l < len; ++l) used |= path[l] == qq;
+                  if (!used) qn = qq;
+                }
+                if (qn < 0) break;
+                q = qn;
+              }
+              if (mx[t1] + mx[t2] < before) {
+                done = improved = true;
+              } else {
+                for (int l = len - 1; l >= 0; --l) swap_pick(path[l], t1, t2);
+              }
+            }
+            if (done) break;  // counts changed: rescan from the next step
+          }
+        }
+        if (!improved) break;
+        descend();
+      }
+    }
     for (int q = 0; q < nl; ++q) {
       const int part = (p0 + q) % NSPLIT;
       uint16_t v[NBG];
