@@ -52,6 +52,28 @@ V = {
         "    cur = nxt;\n  }\n  if (bad) atomicOr(P.err, 1);\n}",
         "    cur = nxt;\n  }\n  if (bad) atomicOr(P.err, 1);\n  __syncthreads();\n"
         "  if (tid < 9) { unsigned long long t = 0; for (int w = 0; w < NT / 64; ++w) t += s_tm[w][tid]; atomicAdd(tmo + tid, t); }\n}")],
+    # per-phase clocks of k_gather_neo (as lin_timing): items, next records + B1, drain, B3, bottom
+    "neo_timing": [(
+        "  static_assert(SW * NTH >= (MAXB * BS2 + 1) / 2 + 1, \"chunk_drain covers every pair\");\n",
+        "  static_assert(SW * NTH >= (MAXB * BS2 + 1) / 2 + 1, \"chunk_drain covers every pair\");\n"
+        "  __shared__ unsigned long long s_tm[4][16];\n"
+        "  if (threadIdx.x < 64) s_tm[threadIdx.x / 16][threadIdx.x % 16] = 0ull;\n"
+        "  unsigned long long* const tmo = reinterpret_cast<unsigned long long*>(dump);\n"
+        "  if (blockIdx.x == 0 && threadIdx.x == 0) printf(\"neo_timing %llu %llu %llu %llu %llu %llu %llu\\n\", tmo[0], tmo[1], tmo[2], tmo[3], tmo[4], tmo[5], tmo[6]);\n"
+        "  unsigned long long t_prev = __builtin_amdgcn_s_memtime(), r_prev = __builtin_amdgcn_s_memrealtime();\n"
+        "#define FN_T(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if ((threadIdx.x & 63) == 0) atomicAdd(&s_tm[threadIdx.x >> 6][i], t_ - t_prev); t_prev = t_; }\n"), (
+        "  for (int64_t k = 0; k < cnt; ++k) {\n    const int32_t pf2 = load_entry(d2);",
+        "  for (int64_t k = 0; k < cnt; ++k) {\n    FN_T(4);\n"
+        "    { const unsigned long long r_ = __builtin_amdgcn_s_memrealtime(); if ((threadIdx.x & 63) == 0) { atomicAdd(&s_tm[threadIdx.x >> 6][5], 1ull); atomicAdd(&s_tm[threadIdx.x >> 6][6], r_ - r_prev); } r_prev = r_; }\n"
+        "    const int32_t pf2 = load_entry(d2);"), (
+        "    // chunk k+1's records / slots / masks: the item registers are dead here, and these loads are\n",
+        "    FN_T(0);\n    // chunk k+1's records / slots / masks: the item registers are dead here, and these loads are\n"), (
+        "    __syncthreads();  // B1: the chunk is accumulated\n    fa_dv2 dv[SW];",
+        "    __syncthreads();  // B1: the chunk is accumulated\n    FN_T(1);\n    fa_dv2 dv[SW];"), (
+        "    __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics\n    keep_vgprs(dv, dh, dt);\n    d0 = d1;",
+        "    FN_T(2);\n    __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics\n    keep_vgprs(dv, dh, dt);\n    FN_T(3);\n    d0 = d1;"), (
+        "  if (bad) atomicOr(P.err, 1);\n}\n\n// ------------------------------------------------------------------------------ block-owner gather",
+        "  if (bad) atomicOr(P.err, 1);\n  __syncthreads();\n  if (threadIdx.x < 7) { unsigned long long t = 0; for (int w = 0; w < 4; ++w) t += s_tm[w][threadIdx.x]; atomicAdd(tmo + threadIdx.x, t); }\n}\n\n// ------------------------------------------------------------------------------ block-owner gather")],
     # no reference-tensor table reads (constants instead)
     "lin_notab": [(
         "          for (int e = 0; e < BS2; ++e) Bn[e] = Ah0[b1 * BS2 + e];",
