@@ -1,6 +1,9 @@
 """Summarise rocprofv3 --pmc CSV passes (tools/prof_passes.sh) per kernel: mean per dispatch.
-FETCH_SIZE / WRITE_SIZE are in KB; gfx950 FETCH_SIZE counts half of wide streaming reads
-(MI355X_MICROARCH.md §HBM) -- both the raw and the x2-corrected values are printed."""
+FETCH_SIZE / WRITE_SIZE are in KiB (tools/probe/fetch_calib.hip: a 4 GiB read gives FETCH_SIZE =
+2 GiB / 1024 for 16-B, 80-B, u16 and u32 lane loads alike, a 4 GiB 16-B store stream WRITE_SIZE =
+1.003 x 4 GiB / 1024); gfx950 FETCH_SIZE counts half of the bytes read (MI355X_MICROARCH.md §HBM):
+both the raw and the x2-corrected values are printed."""
+KIB = 1024.0
 import csv, glob, os, sys
 from collections import defaultdict
 
@@ -19,9 +22,9 @@ for k, d in acc.items():
         mean = sum(per.values()) / len(per)
         extra = ""
         if c == "FETCH_SIZE":
-            extra = f"  (x2 corrected: {2 * mean / 1e6:.3f} GB)"
+            extra = f"  (x2 corrected: {2 * mean * KIB / 1e9:.3f} GB)"
         if c == "WRITE_SIZE":
-            extra = f"  ({mean / 1e6:.3f} GB)"
+            extra = f"  ({mean * KIB / 1e9:.3f} GB)"
         print(f"  {c:24s} {mean:16.1f}{extra}  [{len(per)} dispatches]")
 
 
@@ -43,7 +46,7 @@ def counter_total(name, kernels=LAUNCH_KERNELS):
 
 
 def traffic_record(root, kernels=LAUNCH_KERNELS):
-    """HBM bytes per assembly launch: sum over the launch's kernels of FETCH_SIZE x 2 + WRITE_SIZE (KB)."""
+    """HBM bytes per assembly launch: sum over the launch's kernels of FETCH_SIZE x 2 + WRITE_SIZE (KiB)."""
     tot = 0.0
     for k, d in acc.items():
         if not any(s in k for s in kernels):
@@ -55,7 +58,7 @@ def traffic_record(root, kernels=LAUNCH_KERNELS):
             for did, v in d[c]:
                 per[did] += v
             mean = sum(per.values()) / len(per)
-            tot += (2.0 if c == "FETCH_SIZE" else 1.0) * mean * 1e3
+            tot += (2.0 if c == "FETCH_SIZE" else 1.0) * mean * KIB
     return tot
 
 
