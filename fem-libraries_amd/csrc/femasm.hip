@@ -2168,18 +2168,18 @@ __global__ __launch_bounds__(256, kGatherWaves) void k_gather(GatherArgs P) {
 // k_gather a chunk's item loads were issued after the previous chunk's stores, so every chunk's
 // compute started only once those stores had drained (and its register spills waited vmcnt(0)).
 // Here every vector-memory operation of the loop is unconditional and of a static count per lane
-// (clamped addresses; lanes past a chunk's items or values repeat a valid load / store of the same
-// value), so the compiler's vmcnt waits count exactly the operations issued after a load, and the
-// loads of chunk k+1 (its entries two chunks ahead, its records / slots / masks one chunk ahead)
-// are issued BEFORE chunk k's stores: the item phase of chunk k+1 waits for its own data only,
-// while chunk k's 27 KB drain behind it (each workgroup keeps two chunks of stores in flight).
-// Per chunk: items (LDS atomics; the reference-tensor table B_ab read one block ahead so the wait
-// for it never includes the previous block's atomics) | barrier | accumulator read into registers
-// | barrier | zero what was read, 16-B non-temporal stores (+ the unpaired head / tail value) |
-// barrier. Chunks are a static contiguous range per workgroup (no chunk counter: its atomic would
-// be a conditional vector-memory operation), XCD-contiguous. Dirichlet diagonals are set after the
-// launch (k_bc_diag), items zero every constrained entry as in k_gather. Plans: <= 256 items per
-// chunk (fa_plan_gather caps a chunk at 256 / NSPLIT adjacency entries for these elements).
+// (clamped addresses; lanes past a chunk's items or values store past the buffer range, which is
+// dropped), so the compiler's vmcnt waits count exactly the operations issued after a load, and the
+// loads of chunk k+1 (entries one chunk earlier still; FUSE: one stage more) are issued BEFORE chunk
+// k's stores: the item phase of chunk k+1 waits for its own data only.
+// Per chunk: items (LDS atomics; the packed reference-tensor block read one block ahead so the wait
+// for it never includes the previous block's atomics) | barrier B1 | exchange every value of the
+// chunk with zero into registers (each lane its own pairs: no second barrier), buffer stores
+// (non-temporal, 16 B per lane, + the unpaired head / tail value) | barrier B3. The chunks come from
+// 8 per-XCD counters (kLinCB; the counter's return is waited with the item loads). Dirichlet
+// diagonals are set after the launch (k_bc_diag), items zero every constrained entry as in k_gather.
+// Plans: <= NT items per chunk (fa_plan_gather caps a chunk at NT / NSPLIT adjacency entries and at
+// lin_maxb blocks for these elements). DESIGN.md §3.2, §3.2b.
 // chunk stores: non-temporal (plain stores measured 53.5 vs 49.8 ms on config E)
 template <typename T>
 __device__ __forceinline__ void lin_store(const T& v, T* p) {
