@@ -41,8 +41,8 @@ V = {
         "#define FA_T(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if ((tid & 63) == 0) atomicAdd(&s_tm[tid >> 6][i], t_ - t_prev); t_prev = t_; }\n"), (
         "    // the id of chunk k + AHEAD\n",
         "    FA_T(6);\n    { const unsigned long long r_ = __builtin_amdgcn_s_memrealtime(); if ((tid & 63) == 0) { atomicAdd(&s_tm[tid >> 6][7], 1ull); atomicAdd(&s_tm[tid >> 6][8], r_ - r_prev); } r_prev = r_; }\n    // the id of chunk k + AHEAD\n"), (
-        "    __syncthreads();  // B1: the chunk is accumulated\n    if (FIX && tid == 0) s_fx[k & 1] = 0u;",
-        "    FA_T(0);\n    __syncthreads();  // B1: the chunk is accumulated\n    FA_T(1);\n    if (FIX && tid == 0) s_fx[k & 1] = 0u;"), (
+        "    __syncthreads();  // B1: the chunk is accumulated\n    // the exchanges at raised",
+        "    FA_T(0);\n    __syncthreads();  // B1: the chunk is accumulated\n    FA_T(1);\n    // the exchanges at raised"), (
         "    if constexpr (FIX) {  // chunk k+1's scale",
         "    FA_T(3);\n    if constexpr (FIX) {  // chunk k+1's scale"), (
         "    if constexpr (FIX) {  // the integer sums back to doubles",
