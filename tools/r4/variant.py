@@ -74,12 +74,6 @@ V = {
         "    FN_T(2);\n    __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics\n    keep_vgprs(dv, dh, dt);\n    FN_T(3);\n    d0 = d1;"), (
         "  if (bad) atomicOr(P.err, 1);\n}\n\n// ------------------------------------------------------------------------------ block-owner gather",
         "  if (bad) atomicOr(P.err, 1);\n  __syncthreads();\n  if (threadIdx.x < 7) { unsigned long long t = 0; for (int w = 0; w < 4; ++w) t += s_tm[w][threadIdx.x]; atomicAdd(tmo + threadIdx.x, t); }\n}\n\n// ------------------------------------------------------------------------------ block-owner gather")],
-    # no reference-tensor table reads (constants instead)
-    "lin_notab": [(
-        "          for (int e = 0; e < BS2; ++e) Bn[e] = Ah0[b1 * BS2 + e];",
-        "          for (int e = 0; e < BS2; ++e) Bn[e] = 0.1 * e + b1;"), (
-        "        for (int e = 0; e < BS2; ++e) Bn[e] = Ah0[b * BS2 + e];",
-        "        for (int e = 0; e < BS2; ++e) Bn[e] = 0.2 * e + b;")],
 }
 
 
