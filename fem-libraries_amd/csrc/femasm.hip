@@ -19,6 +19,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cfloat>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
@@ -95,12 +96,17 @@ static bool pack_ahat(int nn, int td, const std::vector<double>& ahat, std::vect
                       double& nmax) {
   if (td != 2 && td != 3) return false;
   const int w = pk_width(td), lo = pk_low(td), lim = (1 << (w - 1)) - 1;
+  double amax = 0.0;
+  for (double v : ahat) amax = std::max(amax, std::fabs(v));
   for (int D = 1; D <= 100000; ++D) {
     bool ok = true;
     nmax = 0.0;
+    // D * Ahat must be integral up to the rounding of the quadrature sums (a few ulp of the table's
+    // largest entry), not merely close: a near-rational table (another rule) keeps the double table
+    const double tol = 64.0 * DBL_EPSILON * std::max(1.0, amax * D);
     for (double v : ahat) {
       const double n = std::nearbyint(v * D);
-      if (std::fabs(v * D - n) > 1e-9 * std::max(1.0, std::fabs(n)) || std::fabs(n) > lim) {
+      if (std::fabs(v * D - n) > tol || std::fabs(n) > lim) {
         ok = false;
         break;
       }
@@ -236,6 +242,16 @@ __device__ __forceinline__ void store_fence(const double (&v)[N][M]) {
 #pragma unroll
     for (int w = 0; w < M; ++w) asm volatile("" ::"v"(v[u][w]));
 }
+// Outside the hot drains, after a >8-byte store: ONE asm statement uses the stored registers and
+// holds 16 wait states, so no write to them can be scheduled before those have passed (a use in one
+// statement and the nops in another would let the compiler put the write in between). The
+// "memory" clobber orders it after the store. Checked on the shipped code object by
+// tests/test_store_hazard.py (tools/store_hazard.py).
+#define FA_GUARD_NOPS "s_nop 7\n\ts_nop 7"
+#define store_guard1(a) asm volatile(FA_GUARD_NOPS ::"v"(a) : "memory")
+#define store_guard2(a, b) asm volatile(FA_GUARD_NOPS ::"v"(a), "v"(b) : "memory")
+#define store_guard3(a, b, c) asm volatile(FA_GUARD_NOPS ::"v"(a), "v"(b), "v"(c) : "memory")
+#define store_guard4(a, b, c, d) asm volatile(FA_GUARD_NOPS ::"v"(a), "v"(b), "v"(c), "v"(d) : "memory")
 template <int N>
 __device__ __forceinline__ void keep_vgprs(const fa_dv2 (&v)[N], double a, double b) {
 #pragma unroll
@@ -522,9 +538,11 @@ __device__ __noinline__ void damage_stress_ad(double s00, double s11, double s01
                                               double w, double (&sig)[2][2]) {
   if (!(d > 0.0)) {
     const double m2plw = w * (2.0 * m + l), lw = l * w;
-    sig[0][0] = m2plw * s00 + lw * s11;
-    sig[1][1] = m2plw * s11 + lw * s00;
-    sig[0][1] = sig[1][0] = w * m * (s01 + s01);
+    const double a = m2plw * s00 + lw * s11, b = m2plw * s11 + lw * s00, c = w * m * (s01 + s01);
+    sig[0][0] = a;
+    sig[1][1] = b;
+    sig[0][1] = sig[1][0] = c;
+    store_guard3(a, b, c);
     return;
   }
   const double st[4] = {s00, s01, s01, s11};
@@ -540,6 +558,7 @@ __device__ __noinline__ void damage_stress_ad(double s00, double s11, double s01
   sig[1][0] = g[1];
   sig[0][1] = g[2];
   sig[1][1] = g[3];
+  store_guard4(g[0], g[1], g[2], g[3]);
 }
 
 // Reference damage-law tangent "hook" (Voigt xx, yy, xy-engineering), restated from MFEM
@@ -2144,6 +2163,8 @@ __global__ __launch_bounds__(256, kGatherWaves) void k_gather(GatherArgs P) {
         const int t = t0 + 256 * u;
         if (t < np) __builtin_nontemporal_store(v[u], out2 + t);
       }
+      static_assert(SU == 4, "store_guard below");
+      store_guard4(v[0], v[1], v[2], v[3]);
     }
     if (((nv - h) & 1) && tid == 0) __builtin_nontemporal_store(acc[nv - 1], out + nv - 1);
   }
@@ -2232,9 +2253,14 @@ constexpr int FA_LIN_FUSE = 1;  // P1 simplices (fa_assemble_matrix): records fo
 __device__ __forceinline__ double pow2(int e) { return __hiloint2double((e + 1023) << 20, 0); }
 
 // k_gather_lin's chunk schedule: a persistent grid of the resident workgroups pulls chunks from 8
-// per-XCD counters, which deal the chunks in blocks of kLinCB (config E 38.3 vs 38.7 ms with ~32
-// chunks per workgroup in a static range; C 1.23 vs 1.27 ms; block sizes 1 / 4 / 64 within 0.5 %)
-constexpr int kLinCB = 16;
+// per-XCD counters (config E 38.3 vs 38.7 ms with ~32 chunks per workgroup in a static range; C 1.23
+// vs 1.27 ms). Round 5: XCD x walks its own contiguous eighth [x per, (x + 1) per) of the visiting
+// sequence (the plan's Morton order, fa_plan_locality, folded into the chunk arrays by
+// lin_chunk_desc), so the chunks that share a cell's record run on one XCD, close in time, and
+// the record is re-read from that XCD's L2. Dealing blocks of 16 row-order chunks round-robin to the
+// XCDs (round 4) put the three lattice lines of a cell's rows on different XCDs: each record was
+// fetched from beyond the L2 ~9 times (tools/r5/sim_l2.py: 8.7 modelled; 48.3 GB fetched per
+// launch against ~17 GB read once, profiles/r4/final_pmc_E.txt); Morton per XCD models 1.6.
 
 template <int GD, int NN, int NSPLIT, int NT = 256, bool FUSE = false, bool FIX = false>
 __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_lin(GatherArgs P, const uint32_t* __restrict__ zero32,
@@ -2265,12 +2291,12 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
   // neighbouring chunks, which share cells, mostly run on one XCD (their records stay in its L2).
   // 32-bit chunk indices (the host checks nchunks < 2^30): fewer SGPRs in the loop
   const int xc = (int)(blockIdx.x % 8);  // the XCD under round-robin dispatch (speed only)
-  (void)per;
-  // the j-th chunk of XCD counter x (blocks of kLinCB chunks dealt round-robin to the counters,
-  // so the 8 XCDs advance through the rows together and the chunks in flight stay close)
+  // the j-th chunk of XCD counter x: position x * per + j of the visiting sequence (past the XCD's
+  // eighth: nchunks, a descriptor of no entries)
   unsigned int* const lctr = reinterpret_cast<unsigned int*>(P.ctr) + 32 * xc;
+  const unsigned int uper = (unsigned int)per, unc = (unsigned int)P.nchunks;
   auto chunk_of = [&](unsigned int j) -> int32_t {
-    return (int32_t)min((j / kLinCB * 8u + (unsigned)xc) * kLinCB + j % kLinCB, 0x7FFFFFFFu);
+    return (int32_t)(j < uper ? min((unsigned)xc * uper + j, unc) : unc);
   };
   if (tid == 0) {
     const unsigned int b = atomicAdd(lctr, (unsigned)AHEAD);
@@ -2720,9 +2746,13 @@ __global__ __launch_bounds__(256) void k_neo_records_m(MeshView M, FormView F, c
   };
   auto flush = [&](double* dst, int n) {  // sb[0, n) -> dst, n even, dst 16-B aligned
     wave_sync();
-    const double2* s2 = reinterpret_cast<const double2*>(sb);
-    double2* d2 = reinterpret_cast<double2*>(dst);
-    for (int t = lane; t < n / 2; t += 64) d2[t] = s2[t];
+    const fa_dv2* s2 = reinterpret_cast<const fa_dv2*>(sb);
+    fa_dv2* d2 = reinterpret_cast<fa_dv2*>(dst);
+    for (int t = lane; t < n / 2; t += 64) {
+      const fa_dv2 v = s2[t];
+      d2[t] = v;
+      store_guard1(v);
+    }
     wave_sync();
   };
   const int64_t ntiles = (M.ncells + 63) / 64;
@@ -2824,7 +2854,7 @@ __global__ __launch_bounds__(256) void k_neo_records_m(MeshView M, FormView F, c
 // 2 waves / SIMD (215 VGPRs, no spills in the item loop; 3 waves measured slower: spilled records)
 template <int GD, int NN, int NQ, int NSPLIT>
 __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint32_t* __restrict__ zero32,
-                                                       double* __restrict__ dump) {
+                                                       double* __restrict__ dump, int64_t per) {
   using R = NeoM<GD, NQ>;
   constexpr int NTH = 256;  // threads: 256 items
   constexpr int BS2 = GD * GD, NT = R::NT, NQL = NQ;
@@ -2843,11 +2873,24 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
   __shared__ double s_T[NN * NN * NT];    // [a][b][t]
   dv2* acc2 = reinterpret_cast<dv2*>(acc);
   const int tid = threadIdx.x;
-  // chunk schedule of k_gather_lin (round-interleaved XCD blocks); a locality order maps through corder
-  const int G = gridDim.x;
-  const int64_t pos = (int64_t)(blockIdx.x % 8) * (G / 8) + blockIdx.x / 8;
-  const int64_t cnt = pos < P.nchunks ? (P.nchunks - pos + G - 1) / G : 0;
-  if (cnt == 0) return;
+  // chunk schedule of k_gather_lin (round 5): the resident grid pulls chunks from 8 per-XCD counters,
+  // XCD x walking its eighth of the plan's visiting sequence (lin_chunk_desc's arrays), ids fetched
+  // AHEAD iterations ahead through an LDS ring. (Round 4: ~128 chunks per workgroup in a static
+  // strided range of the Morton order; consecutive iterations were G chunks apart, so a 384-B record
+  // was fetched from beyond the L2 ~5.5 times: 106.5 GB per launch, profiles/r4/final_pmc_Eneo.txt.)
+  constexpr int LOOK = 3, AHEAD = LOOK + 2, RING = 8;
+  __shared__ int32_t s_id[RING];
+  const int xc = (int)(blockIdx.x % 8);
+  unsigned int* const lctr = reinterpret_cast<unsigned int*>(P.ctr) + 32 * xc;
+  const unsigned int uper = (unsigned int)per, unc = (unsigned int)P.nchunks;
+  auto chunk_of = [&](unsigned int j) -> int32_t {
+    return (int32_t)(j < uper ? min((unsigned)xc * uper + j, unc) : unc);
+  };
+  if (tid == 0) {
+    const unsigned int b = atomicAdd(lctr, (unsigned)AHEAD);
+#pragma unroll
+    for (int t = 0; t < AHEAD; ++t) s_id[t] = chunk_of(b + t);
+  }
   const double* wq = P.tab;
   const double* dphi = P.tab + NQ;  // [q][b][k]
   for (int t = tid; t < NN * NQ * GD; t += NTH) {
@@ -2873,25 +2916,23 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
   }
   for (int t = tid; t < NP2; t += NTH) acc2[t] = dv2{0.0, 0.0};
 
-  const int64_t abase = sload(P.A.indptr, P.A.row_begin);
-  const int64_t nent = P.M.ncells * NN;
   const int32_t* __restrict__ eadj = P.eadj;
   const uint32_t* __restrict__ mk = P.bcmask ? P.bcmask : zero32;
   const uint32_t mkmul = P.bcmask ? 1u : 0u;
-  struct Desc { int64_t b0, b1, a0, a1; };
-  auto desc = [&](int64_t i) -> Desc {  // the workgroup's i-th chunk, clamped to its last: static loads
-    int64_t c = pos + min(i, cnt - 1) * G;
-    if (P.corder) c = sload(P.corder, c);
-    const int64_t r0 = sload(P.row_start, c), r1 = sload(P.row_start, c + 1);
-    return Desc{sload(P.A.indptr, r0), sload(P.A.indptr, r1), sload(P.adj_ptr, r0), sload(P.adj_ptr, r1)};
+  // a chunk (lin_chunk_desc): first block relative to the window, first adjacency entry (clamped
+  // below the entry count), block and entry counts; past the XCD's eighth nb = -1 and no entries
+  struct Desc { int64_t b0, a0; int32_t nb, na; };
+  __syncthreads();  // s_id staged
+  auto desc = [&](int i) -> Desc {
+    const int raw = __builtin_amdgcn_readfirstlane(s_id[i % RING]);
+    const bool ok = raw < (int)P.nchunks;
+    const int c = ok ? raw : (int)P.nchunks - 1;
+    const uint64_t n = (uint64_t)sload(P.chunk_a, (int64_t)P.nchunks + 1 + c);  // block count | entry count << 32
+    return Desc{sload(P.chunk_b, c), sload(P.chunk_a, c), ok ? (int32_t)(uint32_t)n : -1, ok ? (int32_t)(n >> 32) : 0};
   };
   const int item = tid;
   const int jit = item / NSPLIT, part = item % NSPLIT;
-  auto entry_of = [&](const Desc& d) -> int64_t {
-    const int na = (int)(d.a1 - d.a0);
-    int64_t e = d.a0 + min(jit, max(na - 1, 0));
-    return min(max(e, (int64_t)0), nent - 1);
-  };
+  auto entry_of = [&](const Desc& d) -> int64_t { return d.a0 + min(jit, max(d.na - 1, 0)); };
   auto load_entry = [&](const Desc& d) -> int32_t { return eadj[entry_of(d)]; };
   // the head's S and s_c (NT + 1 values; its padding is not loaded); slots two per register
   constexpr int HL = NT + 1, NSL = (NBG + 1) / 2;
@@ -2931,13 +2972,15 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the prologue's loads (see k_gather_lin)
   __syncthreads();                     // tables and accumulator staged
   typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
-  for (int64_t k = 0; k < cnt; ++k) {
+  for (int k = 0; d0.nb >= 0; ++k) {
+    unsigned int rn = 0u;  // the id of chunk k + AHEAD (atomicInc: see k_gather_lin)
+    if (tid == 0) rn = atomicInc(lctr, 0xFFFFFFFFu);
     const int32_t pf2 = load_entry(d2);  // chunk k+2's entry ids
-    const Desc d3 = desc(k + 3);
-    const int64_t off = (d0.b0 - abase) * BS2;
+    const Desc d3 = desc(k + LOOK);
+    const int64_t off = d0.b0 * BS2;
     const int h = (int)(off & 1);
-    const int nb = (int)(d0.b1 - d0.b0);
-    const bool valid = jit < (int)(d0.a1 - d0.a0);
+    const int nb = d0.nb;
+    const bool valid = jit < d0.na;
     {
       const int aloc = pf0 % NN;
       const uint32_t rowm = (cur.mask >> (aloc * GD)) & ((1u << GD) - 1);
@@ -3022,6 +3065,8 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
     chunk_drain<SW, NTH>(acc, h, nb * BS2, P.A.data + off, tid, dv, dh, dt);
     __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics
     keep_vgprs(dv, dh, dt);
+    // chunk k + AHEAD's id, read at iteration k + AHEAD - LOOK (after later barriers)
+    if (tid == 0) s_id[(k + AHEAD) % RING] = chunk_of(rn);
     d0 = d1;
     d1 = d2;
     d2 = d3;
@@ -3256,6 +3301,7 @@ __global__ __launch_bounds__(256, 3) void k_gather_own(GatherArgs P) {
           const int t = t0 + 256 * u;
           if (t < np) __builtin_nontemporal_store(vv[u], out2 + t);
         }
+        store_guard4(vv[0], vv[1], vv[2], vv[3]);
       }
       if (((nv - h) & 1) && tid == 0) __builtin_nontemporal_store(s_out[nv - 1], out + nv - 1);
     }
@@ -3453,6 +3499,109 @@ extern "C" int fa_sparsity_fill(const fa_mesh* mesh, const fa_adjacency* adj, co
 // ------------------------------------------------------------------------------------ gather plan
 // slot map: thread per row node; for each adjacency entry of the row and each column node of the
 // cell, the position of that column in the row (binary search once, at plan time)
+// ------------------------------------------------------------------------------ pattern check
+static int scratch_alloc(void** p, size_t bytes, hipStream_t s);
+// fa_check_pattern: the sparsity pattern and the node -> cell adjacency are built with rocPRIM sorts
+// and scans (whose gfx950 code the library does not control, tools/store_hazard.py); this validates
+// both on the device. One thread per row: indptr monotone, columns in range and strictly increasing;
+// adjacency entries of row r sorted, unique and at a dofmap position holding node r; every node of
+// every adjacent cell found in the row (its block marked in `hit`); then every block marked (no
+// column that no cell needs). Error bits: 1 indptr, 2 columns, 4 missing pair, 8 extra column,
+// 32 adjacency.
+__global__ void k_check_pattern(MeshView M, const int64_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj_idx,
+                                const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+                                int64_t nblocks, uint8_t* __restrict__ hit, int* err) {
+  const int nn = M.nn;
+  const int64_t nent = M.ncells * nn;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < M.nnodes; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b0 = indptr[r], b1 = indptr[r + 1];
+    if (b1 < b0 || b0 < 0 || b1 > nblocks) {
+      atomicOr(err, 1);
+      continue;
+    }
+    int e = 0;
+    for (int64_t k = b0; k < b1; ++k) {
+      const int32_t c = indices[k];
+      if (c < 0 || c >= M.nnodes || (k > b0 && indices[k - 1] >= c)) e |= 2;
+    }
+    const int64_t j0 = adj_ptr[r], j1 = adj_ptr[r + 1];
+    if (j1 < j0 || j0 < 0 || j1 > nent) e |= 32;
+    for (int64_t j = j0; j < j1 && !(e & 32); ++j) {
+      const int32_t p = adj_idx[j];
+      if (p < 0 || p >= nent || M.cells[p] != r || (j > j0 && adj_idx[j - 1] >= p)) {
+        e |= 32;
+        break;
+      }
+      const int64_t c = p / nn;
+      for (int b = 0; b < nn; ++b) {
+        const int32_t col = M.cells[c * nn + b];
+        int64_t lo = b0, hi = b1 - 1, f = -1;
+        while (lo <= hi) {
+          const int64_t mid = (lo + hi) >> 1;
+          const int32_t v = indices[mid];
+          if (v == col) { f = mid; break; }
+          if (v < col) lo = mid + 1; else hi = mid - 1;
+        }
+        if (f < 0) e |= 4;
+        else hit[f] = 1;
+      }
+    }
+    if (e) atomicOr(err, e);
+  }
+}
+__global__ void k_check_hits(const uint8_t* __restrict__ hit, int64_t n, int* err) {
+  int e = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (!hit[i]) e = 8;
+  if (e) atomicOr(err, e);
+}
+
+extern "C" int fa_check_pattern(const fa_mesh* mesh, const fa_adjacency* adj, const int64_t* indptr,
+                                const int32_t* indices, int64_t nblocks, void* stream) {
+  int rc = check_mesh(mesh);
+  if (rc) return rc;
+  if (!adj || !adj->ptr || !adj->idx || !indptr || (!indices && nblocks > 0)) return fail(FA_E_ARG, "null argument");
+  if (nblocks < 0) return fail(FA_E_ARG, "negative block count");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = mesh->nnodes;
+  int64_t h[4] = {0, 0, 0, 0};
+  HIP_TRY(hipMemcpyAsync(&h[0], indptr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&h[1], indptr + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&h[2], adj->ptr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&h[3], adj->ptr + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  MeshView M{mesh->cells, mesh->geom, mesh->x, mesh->ncells, mesh->nnodes, mesh->nn, mesh->nv, mesh->gdim};
+  int* derr = nullptr;
+  uint8_t* hit = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&derr, sizeof(int), s));
+  HIP_TRY(hipMemsetAsync(derr, 0, sizeof(int), s));
+  if ((rc = scratch_alloc((void**)&hit, (size_t)std::max<int64_t>(nblocks, 1), s))) return rc;
+  HIP_TRY(hipMemsetAsync(hit, 0, (size_t)std::max<int64_t>(nblocks, 1), s));
+  if (n > 0) {
+    k_check_pattern<<<grid_for(n), 256, 0, s>>>(M, adj->ptr, adj->idx, indptr, indices, nblocks, hit, derr);
+    LAUNCH_CHECK();
+  }
+  if (nblocks > 0) {
+    k_check_hits<<<grid_for(nblocks), 256, 0, s>>>(hit, nblocks, derr);
+    LAUNCH_CHECK();
+  }
+  int herr = 0;
+  HIP_TRY(hipMemcpyAsync(&herr, derr, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipFreeAsync(hit, s));
+  HIP_TRY(hipFreeAsync(derr, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (h[0] != 0 || h[1] != nblocks)
+    return fail(FA_E_PATTERN, "pattern: indptr[0] = %lld, indptr[nnodes] = %lld for %lld blocks", (long long)h[0],
+                (long long)h[1], (long long)nblocks);
+  if (h[2] != 0 || h[3] != mesh->ncells * mesh->nn)
+    return fail(FA_E_PATTERN, "adjacency: ptr[0] = %lld, ptr[nnodes] = %lld for %lld entries", (long long)h[2],
+                (long long)h[3], (long long)(mesh->ncells * mesh->nn));
+  if (herr)
+    return fail(FA_E_PATTERN, "pattern check failed (bits %d:%s%s%s%s%s)", herr, (herr & 1) ? " indptr" : "",
+                (herr & 2) ? " columns out of range or unsorted" : "", (herr & 4) ? " a cell's (row, column) pair missing" : "",
+                (herr & 8) ? " a column no cell needs" : "", (herr & 32) ? " adjacency" : "");
+  return FA_OK;
+}
+
 __global__ void k_build_slots(MeshView M, const int64_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj_idx,
                               const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
                               uint16_t* __restrict__ slots, int* err) {
@@ -3518,14 +3667,17 @@ extern "C" int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const
 // (chunk, quarter).
 // Positional plans (eperm != NULL): position jj of a chunk holds entry eperm[a0 + jj]; the plain
 // map is read from src and written by position, with chunk-relative block positions.
-// alternating-path moves of the slot order search (k_order_slots): rounds and lanes per chain
+// alternating-path moves of the slot order search (k_order_slots): rounds (with FA_PLAN_ORDER_SEARCH)
+// and lanes per chain. Opt-in since round 5: on config E they took the plan from 1.7 to 20 s for
+// 37.6 -> 37.4 ms per assembly (break-even after ~90,000 assemblies; the reference assembles J a few
+// times per Newton solve)
 constexpr int kKempeRounds = 4;
 constexpr int kKempeLen = 6;
 template <int NN, int NSPLIT>
 __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64_t* __restrict__ indptr,
                               const int64_t* __restrict__ adj_ptr, int64_t nchunks, int groups_per_chunk,
                               uint16_t* __restrict__ slots, const uint16_t* __restrict__ src,
-                              const uint16_t* __restrict__ eperm) {
+                              const uint16_t* __restrict__ eperm, int rounds) {
   constexpr int NBG = NN / NSPLIT, Q = 16;
   const int64_t total = nchunks * groups_per_chunk;
   for (int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gid < total;
@@ -3626,9 +3778,9 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
     // too, and so on (at most kKempeLen lanes). A chain is kept when the two steps' passes drop,
     // otherwise undone; then the descent runs again. (config E: passes 1.30 x the per-quarter bound
     // max(steps, largest residue count) after the descent alone; tools/r4/plan_stats.py)
-    if constexpr (kKempeRounds > 0 && NBG > 1) {
+    if constexpr (NBG > 1) {
       auto res_at = [&](int q, int t) { return (int)res[q][pick[q][t]]; };
-      for (int round = 0; round < kKempeRounds; ++round) {
+      for (int round = 0; round < rounds; ++round) {
         bool improved = false;
         for (int t1 = 0; t1 < NBG; ++t1) {
           for (int r = 0; r < 16; ++r) {
@@ -3785,6 +3937,7 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   // for a plan whose chunks could hold 1024 blocks or more
   if (plan->max_blocks >= 1024 || gather_maxb(false, mesh->gdim * mesh->gdim) >= 1024) return FA_OK;
   const int groups = (kGatherMaxAdj * ns + 15) / 16;
+  const int rounds = (plan->cell_flags & FA_PLAN_ORDER_SEARCH) ? kKempeRounds : 0;
   hipStream_t s = (hipStream_t)stream;
   const int64_t total = plan->nchunks * groups;
   uint16_t* sl = const_cast<uint16_t*>(plan->slots);
@@ -3806,7 +3959,7 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
       k_plan_perm<NN_, NS_><<<grid_for(plan->nchunks), 64, 0, s>>>(plan->row_start, A->indptr, adj->ptr,      \
                                                                    adj->idx, plan->nchunks, src, eperm, eadj);   \
     k_order_slots<NN_, NS_><<<grid_for(total), 256, 0, s>>>(plan->row_start, A->indptr, adj->ptr, plan->nchunks, \
-                                                            groups, sl, src, eperm);                           \
+                                                            groups, sl, src, eperm, rounds);                   \
   } while (0)
   bool ok = true;
   if (mesh->nn == 3 && ns == 1) ORD(3, 1);
@@ -4352,18 +4505,6 @@ __global__ void k_chunk_desc(const int64_t* __restrict__ row_start, int64_t nchu
   }
 }
 
-// k_gather_neo's grid: about kNeoChunksPerWg chunks per workgroup in a static range, never fewer
-// workgroups than are resident (config E-neo, alternating on one box: 74.0-74.3 ms at 64 times the
-// resident count against 75.5-76.9 at 1 time). k_gather_lin's dynamic schedule runs the resident grid.
-constexpr int kNeoChunksPerWg = 128;
-template <typename K>
-static int64_t neo_grid(K kernel, int64_t nchunks, int block, int per_wg = kNeoChunksPerWg) {
-  const int64_t g0 = gather_grid(kernel, nchunks, block);
-  const int64_t per = (nchunks + 7) / 8;
-  const int64_t g = std::max<int64_t>(g0, nchunks / per_wg / 8 * 8);
-  return std::min<int64_t>(std::min<int64_t>(8 * per, g), kMaxBlocks);
-}
-
 static int chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
   int rc;
   if (P.nchunks >= (1ll << 31)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks (>= 2^31)", (long long)P.nchunks);
@@ -4382,20 +4523,24 @@ static int chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
 // chunk_a[c] = its first adjacency entry (clamped below the entry count, so a lane's entry load is
 // always in range) and chunk_a[nchunks + 1 + c] = block count | entry count << 32: three scalar
 // loads per chunk, no dependent level, and fewer pointers live in the kernel's loop
+// Position i of the arrays describes chunk seq[i] (the plan's visiting order) or chunk i (seq NULL).
 __global__ void k_lin_chunk_desc(const int64_t* __restrict__ row_start, int64_t nchunks, const int64_t* __restrict__ indptr,
                                  int64_t row_begin, const int64_t* __restrict__ adj_ptr, int64_t nent,
-                                 int64_t* __restrict__ cb, int64_t* __restrict__ ca) {
+                                 const int32_t* __restrict__ seq, int64_t* __restrict__ cb, int64_t* __restrict__ ca) {
   const int64_t base = indptr[row_begin];
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = seq ? (int64_t)seq[i] : i;
     const int64_t r0 = row_start[c], r1 = row_start[c + 1];
     const int64_t b0 = indptr[r0], a0 = adj_ptr[r0];
-    cb[c] = b0 - base;
-    ca[c] = min(a0, max(nent - 1, (int64_t)0));
-    ca[nchunks + 1 + c] = (int64_t)((uint64_t)(uint32_t)(indptr[r1] - b0) | ((uint64_t)(uint32_t)(adj_ptr[r1] - a0) << 32));
+    cb[i] = b0 - base;
+    ca[i] = min(a0, max(nent - 1, (int64_t)0));
+    ca[nchunks + 1 + i] = (int64_t)((uint64_t)(uint32_t)(indptr[r1] - b0) | ((uint64_t)(uint32_t)(adj_ptr[r1] - a0) << 32));
   }
 }
 
-static int lin_chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
+// the chunk arrays of the persistent per-XCD schedule (k_gather_lin, k_gather_neo) in the order seq
+// (NULL: row order), and the XCD counters (zeroed)
+static int lin_chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s, const int32_t* seq) {
   int rc;
   if (P.nchunks >= (1ll << 30)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks (>= 2^30)", (long long)P.nchunks);
   if ((rc = scratch_alloc((void**)buf, sizeof(int64_t) * (3 * (P.nchunks + 1) + 128), s))) return rc;
@@ -4404,7 +4549,7 @@ static int lin_chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s) {
   P.ctr = reinterpret_cast<unsigned long long*>(*buf + 3 * (P.nchunks + 1));  // 8 counters, 128 B apart
   HIP_TRY(hipMemsetAsync(P.ctr, 0, 1024, s));
   k_lin_chunk_desc<<<grid_for(P.nchunks), 256, 0, s>>>(P.row_start, P.nchunks, P.A.indptr, P.A.row_begin, P.adj_ptr,
-                                                       P.M.ncells * P.M.nn, *buf, *buf + (P.nchunks + 1));
+                                                       P.M.ncells * P.M.nn, seq, *buf, *buf + (P.nchunks + 1));
   LAUNCH_CHECK();
   return FA_OK;
 }
@@ -4532,9 +4677,12 @@ static int launch_gather_neo(GatherArgs P, const int8_t* bc, hipStream_t s, cons
     uint32_t* zero32 = nullptr;
     double* dump = nullptr;
     if ((rc = lin_scratch(&zero32, &dump))) return rc;
-    const int64_t grid = neo_grid(k_gather_neo<GD, NN, NQ, NSPLIT>, P.nchunks, 256);
-    k_gather_neo<GD, NN, NQ, NSPLIT><<<(unsigned)grid, 256, 0, s>>>(P, zero32, dump);
+    int64_t* ldesc = nullptr;
+    if ((rc = lin_chunk_desc(P, &ldesc, s, P.corder))) return rc;
+    const int64_t grid = gather_grid(k_gather_neo<GD, NN, NQ, NSPLIT>, P.nchunks, 256);
+    k_gather_neo<GD, NN, NQ, NSPLIT><<<(unsigned)grid, 256, 0, s>>>(P, zero32, dump, (P.nchunks + 7) / 8);
     LAUNCH_CHECK();
+    HIP_TRY(hipFreeAsync(ldesc, s));
     if (bc) {  // Dirichlet diagonals (dolfinx set_diagonal) of the plan's rows
       k_bc_diag<GD><<<grid_for((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
       LAUNCH_CHECK();
@@ -4576,10 +4724,12 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   if (P.plan_maxb > gather_maxb(false, GD * GD))
     return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, this form's kernel %d: plan with fa_plan_gather_form",
                 P.plan_maxb, gather_maxb(false, GD * GD));
-  // the chunk visiting order (fa_plan_locality) pays where the records are large (neo-Hookean,
-  // 342 -> 328 ms on config E-neo); the 80-B linear records stay in L2 in row order (E: 50.0 vs
-  // 51.5 ms in Morton order)
+  // the chunk visiting order (fa_plan_locality): k_gather_lin walks it per XCD (lin_chunk_desc);
+  // the generic k_gather keeps row order (its static grid measured 50.0 vs 51.5 ms on config E in
+  // Morton order, round 2)
+  const int32_t* seq = P.corder;
   P.corder = nullptr;
+  const int64_t per8 = (P.nchunks + 7) / 8;
   if constexpr (MAT == MAT_LINU && R::SIMP && NN == GD + 1 && NN % NSPLIT == 0 && FA_LIN_FUSE) {
     // P1 simplices through fa_assemble_matrix: k_gather_lin forms the records itself (FUSE)
     constexpr int LNT = lin_threads(GD, NN);
@@ -4605,13 +4755,13 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       if (!nm) P.nodemask = reinterpret_cast<const uint8_t*>(zero32);  // a valid address (mask scaled by 0)
       P.fixc = lin_fix_bound(GD, NN, P.rlm, P.trc, P.amax);
       int64_t* ldesc = nullptr;
-      if ((rc = lin_chunk_desc(P, &ldesc, s))) return rc;
+      if ((rc = lin_chunk_desc(P, &ldesc, s, seq))) return rc;
       if (P.fix) {
         const int64_t grid = gather_grid(k_gather_lin<GD, NN, NSPLIT, LNT, true, true>, P.nchunks, LNT);
-        k_gather_lin<GD, NN, NSPLIT, LNT, true, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
+        k_gather_lin<GD, NN, NSPLIT, LNT, true, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, per8);
       } else {
         const int64_t grid = gather_grid(k_gather_lin<GD, NN, NSPLIT, LNT, true>, P.nchunks, LNT);
-        k_gather_lin<GD, NN, NSPLIT, LNT, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
+        k_gather_lin<GD, NN, NSPLIT, LNT, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, per8);
       }
       LAUNCH_CHECK();
       HIP_TRY(hipFreeAsync(ldesc, s));
@@ -4663,13 +4813,13 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       if ((rc = lin_scratch(&zero32, &dump))) return rc;
       P.fixc = lin_fix_bound(GD, NN, rr, P.trc, P.pkmax);  // records scaled by 1 / sqrt(D): |N| bounds
       int64_t* ldesc = nullptr;
-      if ((rc = lin_chunk_desc(P, &ldesc, s))) return rc;
+      if ((rc = lin_chunk_desc(P, &ldesc, s, seq))) return rc;
       if (P.fix) {
         const int64_t grid = gather_grid(k_gather_lin<GD, NN, NSPLIT, LNT, false, true>, P.nchunks, LNT);
-        k_gather_lin<GD, NN, NSPLIT, LNT, false, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
+        k_gather_lin<GD, NN, NSPLIT, LNT, false, true><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, per8);
       } else {
         const int64_t grid = gather_grid(k_gather_lin<GD, NN, NSPLIT, LNT>, P.nchunks, LNT);
-        k_gather_lin<GD, NN, NSPLIT, LNT><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, 0);
+        k_gather_lin<GD, NN, NSPLIT, LNT><<<(unsigned)grid, LNT, 0, s>>>(P, zero32, dump, per8);
       }
       LAUNCH_CHECK();
       HIP_TRY(hipFreeAsync(ldesc, s));
@@ -4884,6 +5034,10 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
   DevTables T;
   if ((rc = get_tables(mesh->cell_type, mesh->degree, form->qdeg, &T))) return rc;
   hipStream_t s = (hipStream_t)stream;
+  // FA_CHECK_ERRORS: the pattern and adjacency are validated on the device first (fa_check_pattern)
+  if ((flags & FA_CHECK_ERRORS) && adj && adj->ptr && adj->idx &&
+      (rc = fa_check_pattern(mesh, adj, A->indptr, A->indices, A->nblocks, stream)))
+    return rc;
   MeshView M{mesh->cells, mesh->geom, mesh->x, mesh->ncells, mesh->nnodes, mesh->nn, mesh->nv, mesh->gdim};
   BsrView Av{A->indptr, A->indices, A->data, wb, we};
   static int* derr = nullptr;  // per-process device error word (sticky until read)
@@ -5358,6 +5512,8 @@ __global__ __launch_bounds__(256) void k_bsr_mult(BsrView A, const double* __res
     }
 #pragma unroll
     for (int i = 0; i < BS; ++i) y[r * BS + i] = acc[i];
+    if constexpr (BS == 2) store_guard2(acc[0], acc[1]);
+    else store_guard3(acc[0], acc[1], acc[2]);
   }
 }
 

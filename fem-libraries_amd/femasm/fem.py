@@ -22,21 +22,9 @@ from . import _lib
 from .la import MatrixCSR
 from .mesh import CellType, Mesh, NVERTS
 
-# basix reference sub-entities (edges as vertex pairs, hex faces as (v0, v1, v2))
-_EDGES = {
-    CellType.triangle: ((1, 2), (0, 2), (0, 1)),
-    CellType.tetrahedron: ((2, 3), (1, 3), (1, 2), (0, 3), (0, 2), (0, 1)),
-    CellType.quadrilateral: ((0, 1), (0, 2), (1, 3), (2, 3)),
-    CellType.hexahedron: ((0, 1), (0, 2), (0, 4), (1, 3), (1, 5), (2, 3), (2, 6), (3, 7), (4, 5), (4, 6), (5, 7), (6, 7)),
-}
-_HEX_FACES = ((0, 1, 2, 3), (0, 1, 4, 5), (0, 2, 4, 6), (1, 3, 5, 7), (2, 3, 6, 7), (4, 5, 6, 7))
+from .mesh import EDGES as _EDGES, HEX_FACES as _HEX_FACES, REF_VERTS as _REF_VERTS  # basix sub-entities
+
 _HEX_FACE_SPAN = ((0, 1, 2), (0, 1, 4), (0, 2, 4), (1, 3, 5), (2, 3, 6), (4, 5, 6))
-_REF_VERTS = {
-    CellType.triangle: ((0, 0), (1, 0), (0, 1)),
-    CellType.tetrahedron: ((0, 0, 0), (1, 0, 0), (0, 1, 0), (0, 0, 1)),
-    CellType.quadrilateral: ((0, 0), (1, 0), (0, 1), (1, 1)),
-    CellType.hexahedron: tuple((b & 1, (b >> 1) & 1, (b >> 2) & 1) for b in range(8)),
-}
 
 
 def is_simplex(ct) -> bool:
@@ -343,6 +331,55 @@ def locate_dofs_geometrical(V: FunctionSpace, marker) -> torch.Tensor:
     return torch.nonzero(marker(xn.T), as_tuple=False).reshape(-1)
 
 
+def _closure_nodes(ct, p: int, S) -> list:
+    """Local nodes (basix order) in the closure of the reference sub-entity with local vertices S:
+    simplices, barycentric coordinates of the vertices outside S vanish; tensor cells, the node lies
+    on every coordinate plane all vertices of S share."""
+    ct = CellType(ct)
+    X = reference_nodes(ct, p)
+    RV = np.array(_REF_VERTS[ct], dtype=np.float64)
+    on = np.ones(X.shape[0], dtype=bool)
+    if is_simplex(ct):
+        lam = np.concatenate([1.0 - X.sum(1, keepdims=True), X], axis=1)  # [nn, nv]
+        for v in range(RV.shape[0]):
+            if v not in S:
+                on &= np.abs(lam[:, v]) < 1e-12
+    else:
+        for d in range(RV.shape[1]):
+            vals = {RV[v, d] for v in S}
+            if len(vals) == 1:
+                on &= np.abs(X[:, d] - vals.pop()) < 1e-12
+    return [int(j) for j in np.nonzero(on)[0]]
+
+
+def locate_dofs_topological(V: FunctionSpace, entity_dim: int, entities) -> torch.Tensor:
+    """dolfinx.fem.locate_dofs_topological: the nodes (block dofs) in the closure of the given
+    entities of dimension entity_dim (ids of femasm.mesh.entities; vertex indices for dim 0).
+    Closure semantics as dolfinx: a vertex carries only its own node, an edge its vertices' and its
+    interior nodes, a facet every node on it. The reference selects with entity_dim 0
+    (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:637-638, :661-662), which for P >= 2 constrains
+    the vertex nodes of the plane only. Returns sorted node indices (int64)."""
+    from . import mesh as fmesh
+
+    m = V.mesh
+    ents = torch.as_tensor(entities, device=m.device).to(torch.int64).reshape(-1)
+    _, cell_ents = fmesh.entities(m, entity_dim) if entity_dim < m.tdim else \
+        (None, torch.arange(m.num_cells, device=m.device, dtype=torch.int64).reshape(-1, 1))
+    nent = int(cell_ents.max()) + 1 if cell_ents.numel() else 0
+    mark = torch.zeros(max(nent, int(ents.max()) + 1 if ents.numel() else 0), dtype=torch.bool, device=m.device)
+    mark[ents] = True
+    dm = V.dofmap.to(torch.int64)
+    out = []
+    for i, S in enumerate(fmesh.sub_entities(m.cell_type, entity_dim)):
+        loc = torch.tensor(_closure_nodes(m.cell_type, V.degree, S), dtype=torch.int64, device=m.device)
+        hit = mark[cell_ents[:, i]]
+        if bool(hit.any()):
+            out.append(dm[hit][:, loc].reshape(-1))
+    if not out:
+        return torch.zeros(0, dtype=torch.int64, device=m.device)
+    return torch.unique(torch.cat(out))
+
+
 def dirichletbc(value, nodes: torch.Tensor, V: FunctionSpace, components=None) -> DirichletBC:
     """Constrain all (or the given) components of `nodes` to `value` (a scalar or a bs-vector)."""
     bs = V.bs
@@ -491,9 +528,20 @@ def _fa_form(a) -> _lib.fa_form:
     return f
 
 
-def create_matrix(a, max_part_bytes: int | None = None) -> MatrixCSR:
+def check_pattern(V: FunctionSpace, indptr: torch.Tensor, indices: torch.Tensor):
+    """Validate a pattern of V and V's adjacency on the device (fa_check_pattern): sorted unique
+    in-range columns, monotone indptr, exactly the node pairs of the cells. Raises FemasmError."""
+    fm = V._fa_mesh()
+    adj = V._fa_adjacency()
+    _lib.check(_lib.load().fa_check_pattern(ctypes.byref(fm), ctypes.byref(adj), indptr.data_ptr(), indices.data_ptr(),
+                                            int(indices.numel()), _lib.stream_handle(V.mesh.device)),
+               "fa_check_pattern")
+
+
+def create_matrix(a, max_part_bytes: int | None = None, check: bool = False) -> MatrixCSR:
     """Sparsity pattern of the bilinear form (all node pairs of every cell), built on the GPU
-    (dolfinx.fem.petsc.create_matrix, FEniCSx/mechanic2d/asym_elasto_damage_model.cc:688)."""
+    (dolfinx.fem.petsc.create_matrix, FEniCSx/mechanic2d/asym_elasto_damage_model.cc:688).
+    check: validate the pattern and adjacency on the device (fa_check_pattern)."""
     V = a.V
     if V._pattern is None:
         L = _lib.load()
@@ -510,6 +558,8 @@ def create_matrix(a, max_part_bytes: int | None = None) -> MatrixCSR:
                    "fa_sparsity_fill")
         V._pattern = (indptr, indices)
     indptr, indices = V._pattern
+    if check:
+        check_pattern(V, indptr, indices)
     if max_part_bytes is None:
         return MatrixCSR(indptr, indices, V.bs)
     return MatrixCSR(indptr, indices, V.bs, max_part_bytes=max_part_bytes)
@@ -519,14 +569,18 @@ def _fa_bsr(A: MatrixCSR, part: int = 0) -> _lib.fa_bsr:
     return A._fa_bsr(part)
 
 
-def _plan_order(V, fm, adj, fb, plan, sh, eadj=None, order: str = "positional"):
+def _plan_order(V, fm, adj, fb, plan, sh, eadj=None, order: str = "positional", search: bool = False):
     """Bank-conflict-aware LDS order of the affine-simplex gather (fa_plan_order). order:
     "positional" (default) also balances which entries share a 16-lane quarter (one int32 per
-    adjacency entry), "steps" orders each lane's blocks only, "none" keeps the plain slot map."""
+    adjacency entry), "steps" orders each lane's blocks only, "none" keeps the plain slot map.
+    search: also the alternating-path moves (FA_PLAN_ORDER_SEARCH: ~0.5 % faster assemblies on config E
+    for a ~10x longer plan)."""
     if order not in ("positional", "steps", "none"):
         raise ValueError(f"unknown slot order {order!r}")
     if order == "none":
         return None
+    if search:
+        plan.cell_flags |= _lib.FA_PLAN_ORDER_SEARCH
     if order == "positional" and eadj is None:
         eadj = torch.empty(V.mesh.num_cells * V.nn, dtype=torch.int32, device=V.mesh.device)
     if order != "positional":
@@ -585,17 +639,23 @@ def _plan_contrib(V, fm, adj, fb, rs, plan, sh):
 
 def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.FA_LINEAR_ELASTICITY,
                 deterministic: bool = False, owner: bool | None = None, slots: bool = True,
-                order: str = "positional", locality: bool = True):
+                order: str = "positional", locality: bool = True, search: bool = False):
     """Row-chunk plan of the gather kernel of a form kind for one row part of A's pattern (cached
     on V per options). Neo-Hookean forms get their own chunking (fa_plan_gather_form); the other
     kinds share one. deterministic: the LDS-atomic gather's plan (no contribution plan), for
     FA_DETERMINISTIC. owner: the block-owner contribution plan (None: for triangles). slots: the
     per-entry slot map (fa_plan_slots; False: the kernels search the pattern in LDS). order: the
-    slot map's LDS order (_plan_order). locality: Morton chunk order (fa_plan_locality)."""
-    plans = V.__dict__.setdefault("_plans", {})
+    slot map's LDS order (_plan_order). search: the order's alternating-path moves (opt-in).
+    locality: the chunk visiting order (fa_plan_locality: Morton order, walked per XCD)."""
+    if deterministic and owner:
+        raise ValueError("deterministic assembly runs the LDS-atomic gather: owner=True (block-owner plan) "
+                         "cannot be combined with deterministic=True")
     neo = kind == _lib.FA_NEO_HOOKEAN
+    if neo and not (slots and order == "positional"):
+        raise ValueError("the neo-Hookean gather needs positional plans (slots=True, order='positional')")
+    plans = V.__dict__.setdefault("_plans", {})
     contrib = _use_contrib(V, kind, owner) and not deterministic
-    key = (A.indptr.data_ptr(), A.parts[part][0], A.parts[part][1], neo, contrib, slots, order, locality)
+    key = (A.indptr.data_ptr(), A.parts[part][0], A.parts[part][1], neo, contrib, slots, order, locality, search)
     if key not in plans:
         L = _lib.load()
         fm = V._fa_mesh()
@@ -622,7 +682,7 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.
                                        ctypes.byref(plan), sh), "fa_plan_slots")
             # bank-balanced positional order of the LDS adds (affine-simplex elasticity and, with the
             # same column split, the neo-Hookean gather)
-            eadj = _plan_order(V, fm, adj, fb, plan, sh, order=order)
+            eadj = _plan_order(V, fm, adj, fb, plan, sh, order=order, search=search)
         corder = _plan_locality(V, fm, adj, plan, sh, locality)
         plans[key] = (plan, rs, A.indptr, smap, eadj, corder)
         V.__dict__.setdefault("_plan_xver", {})[key] = _coords_version(V.mesh)
@@ -664,6 +724,10 @@ def assemble_matrix(a, bcs=None, diagonal: float = 1.0, A: MatrixCSR | None = No
     kernel found a pattern entry missing (FA_CHECK_ERRORS).
     """
     V = a.V
+    if method not in ("gather", "scatter"):
+        raise ValueError(f"unknown method {method}")
+    if deterministic and method != "gather":
+        raise ValueError("deterministic assembly is a gather mode")
     if A is None:
         A = create_matrix(a)
     L = _lib.load()
@@ -680,14 +744,10 @@ def assemble_matrix(a, bcs=None, diagonal: float = 1.0, A: MatrixCSR | None = No
                 (_lib.FA_CHECK_ERRORS if check else 0)
             rc = L.fa_assemble_matrix(ctypes.byref(fm), ctypes.byref(ff), ctypes.byref(adj), ctypes.byref(gp),
                                       _lib.ptr(marker), float(diagonal), ctypes.byref(fb), flags, sh)
-        elif method == "scatter":
+        else:
             flags = _lib.FA_SCATTER | _lib.FA_ZERO_FIRST | (_lib.FA_CHECK_ERRORS if check else 0)
             rc = L.fa_assemble_matrix(ctypes.byref(fm), ctypes.byref(ff), None, None, _lib.ptr(marker),
                                       float(diagonal), ctypes.byref(fb), flags, sh)
-        else:
-            raise ValueError(f"unknown method {method}")
-        if deterministic and method != "gather":
-            raise ValueError("deterministic assembly is a gather mode")
         _lib.check(rc, "fa_assemble_matrix")
     A._keepalive = (marker, a)
     return A

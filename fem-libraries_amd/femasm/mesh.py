@@ -28,6 +28,46 @@ class CellType(IntEnum):
 GDIM = {CellType.triangle: 2, CellType.quadrilateral: 2, CellType.tetrahedron: 3, CellType.hexahedron: 3}
 NVERTS = {CellType.triangle: 3, CellType.quadrilateral: 4, CellType.tetrahedron: 4, CellType.hexahedron: 8}
 
+# basix reference sub-entities: edges as vertex pairs, faces as vertex tuples (hexahedron faces in
+# the face's own tensor order v0, v1, v2, v3; tetrahedron face i is opposite vertex i)
+EDGES = {
+    CellType.triangle: ((1, 2), (0, 2), (0, 1)),
+    CellType.tetrahedron: ((2, 3), (1, 3), (1, 2), (0, 3), (0, 2), (0, 1)),
+    CellType.quadrilateral: ((0, 1), (0, 2), (1, 3), (2, 3)),
+    CellType.hexahedron: ((0, 1), (0, 2), (0, 4), (1, 3), (1, 5), (2, 3), (2, 6), (3, 7), (4, 5), (4, 6), (5, 7), (6, 7)),
+}
+HEX_FACES = ((0, 1, 2, 3), (0, 1, 4, 5), (0, 2, 4, 6), (1, 3, 5, 7), (2, 3, 6, 7), (4, 5, 6, 7))
+TET_FACES = ((1, 2, 3), (0, 2, 3), (0, 1, 3), (0, 1, 2))
+REF_VERTS = {
+    CellType.triangle: ((0, 0), (1, 0), (0, 1)),
+    CellType.tetrahedron: ((0, 0, 0), (1, 0, 0), (0, 1, 0), (0, 0, 1)),
+    CellType.quadrilateral: ((0, 0), (1, 0), (0, 1), (1, 1)),
+    CellType.hexahedron: tuple((b & 1, (b >> 1) & 1, (b >> 2) & 1) for b in range(8)),
+}
+
+
+def sub_entities(ct, dim: int) -> tuple:
+    """Local vertex tuples of a cell's sub-entities of dimension dim (basix numbering)."""
+    ct = CellType(ct)
+    tdim = GDIM[ct]
+    if dim == 0:
+        return tuple((v,) for v in range(NVERTS[ct]))
+    if dim == tdim:
+        return (tuple(range(NVERTS[ct])),)
+    if dim == 1:
+        return EDGES[ct]
+    if dim == 2 and tdim == 3:
+        return TET_FACES if ct == CellType.tetrahedron else HEX_FACES
+    raise ValueError(f"no sub-entities of dimension {dim} for {ct.name}")
+
+
+def _facet_edges(ct):
+    """Edges of each facet of a 3-D cell, as local vertex pairs (hexahedron faces: the 4 sides, not
+    the diagonals)."""
+    if CellType(ct) == CellType.tetrahedron:
+        return tuple(((f[0], f[1]), (f[0], f[2]), (f[1], f[2])) for f in TET_FACES)
+    return tuple(((f[0], f[1]), (f[0], f[2]), (f[1], f[3]), (f[2], f[3])) for f in HEX_FACES)
+
 
 @dataclass
 class Mesh:
@@ -177,6 +217,85 @@ def read_gmsh(path: str, gdim: int | None = None, device=None) -> Mesh:
     tags = torch.tensor([t for t, _ in elems[et]], dtype=torch.int32)
     m = Mesh(ct, x, cells, tags, None)
     return m.to(device) if device is not None else m
+
+
+def _unique_rows(t: torch.Tensor):
+    """(unique sorted rows of an int64 tensor [n, k], inverse index [n])."""
+    if t.shape[1] == 1:
+        return torch.unique(t[:, 0], return_inverse=True)
+    return torch.unique(t, dim=0, return_inverse=True)
+
+
+def entities(mesh: Mesh, dim: int):
+    """Topology of dimension dim (dolfinx mesh.topology.create_entities): (vertex tuples of the
+    entities [ne, k] int64, each cell's entity ids [ncells, n_local] int64). Entities are numbered in
+    the lexicographic order of their sorted vertex tuples; dim 0 entities are the vertices themselves
+    (mesh.x rows). Cached on the mesh."""
+    cache = mesh.__dict__.setdefault("_entities", {})
+    if dim in cache:
+        return cache[dim]
+    c = mesh.cells.to(torch.int64)
+    if dim == 0:
+        ent = torch.arange(mesh.num_vertices, device=c.device, dtype=torch.int64).reshape(-1, 1)
+        out = (ent, c)
+    else:
+        S = torch.tensor(sub_entities(mesh.cell_type, dim), dtype=torch.int64, device=c.device)  # [nl, k]
+        tup = torch.sort(c[:, S], dim=-1).values  # [nc, nl, k]
+        ent, inv = _unique_rows(tup.reshape(-1, S.shape[1]))
+        out = (ent.reshape(-1, S.shape[1]), inv.reshape(c.shape[0], S.shape[0]))
+    cache[dim] = out
+    return out
+
+
+def exterior_facets(mesh: Mesh) -> torch.Tensor:
+    """Facet ids (entities(mesh, tdim - 1)) that belong to exactly one cell (dolfinx
+    exterior_facet_indices on one process)."""
+    _, cf = entities(mesh, mesh.tdim - 1)
+    cnt = torch.bincount(cf.reshape(-1), minlength=int(cf.max()) + 1 if cf.numel() else 0)
+    return torch.nonzero(cnt == 1, as_tuple=False).reshape(-1)
+
+
+def locate_entities_boundary(mesh: Mesh, dim: int, marker) -> torch.Tensor:
+    """dolfinx.mesh.locate_entities_boundary: the entities of dimension dim attached to an exterior
+    facet (the facets themselves, or their edges / vertices) whose vertices ALL satisfy
+    marker(x[gdim, n]). Returns sorted entity ids (int32) of entities(mesh, dim); for dim 0 these are
+    vertex indices. The reference calls it with dim 0 (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:627-636,
+    :651-660)."""
+    tdim = mesh.tdim
+    if not 0 <= dim < tdim:
+        raise ValueError(f"boundary entities have dimension 0 .. {tdim - 1}, not {dim}")
+    fverts, _ = entities(mesh, tdim - 1)
+    ext = exterior_facets(mesh)
+    dev = mesh.x.device
+    if dim == tdim - 1:
+        cand = ext
+        cand_verts = fverts[ext]
+    elif dim == 0:
+        cand = torch.unique(fverts[ext].reshape(-1))
+        cand_verts = cand.reshape(-1, 1)
+    else:  # dim 1 of a 3-D mesh: the edges of the exterior facets
+        # an exterior facet's vertices in its cell's local order give its edges (hexahedron faces:
+        # the sides only); locate each exterior facet in one of its cells
+        _, cf = entities(mesh, tdim - 1)
+        c = mesh.cells.to(torch.int64)
+        flat = cf.reshape(-1)
+        is_ext = torch.zeros(fverts.shape[0], dtype=torch.bool, device=dev)
+        is_ext[ext] = True
+        hit = torch.nonzero(is_ext[flat], as_tuple=False).reshape(-1)
+        cell, lf = hit // cf.shape[1], hit % cf.shape[1]
+        FE = torch.tensor(_facet_edges(mesh.cell_type), dtype=torch.int64, device=dev)  # [nf, ne, 2]
+        ev = c[cell[:, None, None], FE[lf]]  # [n, ne, 2]
+        ev = torch.sort(ev.reshape(-1, 2), dim=-1).values
+        everts, _ = entities(mesh, 1)
+        # ids of these edges in entities(mesh, 1): search the sorted unique tuples
+        key_all = everts[:, 0] * mesh.num_vertices + everts[:, 1]
+        key = torch.unique(ev[:, 0] * mesh.num_vertices + ev[:, 1])
+        cand = torch.searchsorted(key_all, key)
+        cand_verts = everts[cand]
+    ok = marker(mesh.x.T)
+    ok = torch.as_tensor(ok, device=dev).to(torch.bool)
+    keep = ok[cand_verts].all(dim=1)
+    return cand[keep].to(torch.int32)
 
 
 def locate_vertices(mesh: Mesh, marker) -> torch.Tensor:

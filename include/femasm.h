@@ -64,8 +64,9 @@ extern "C" {
 #define FA_SCATTER 0x1       /* element-scatter with FP64 atomics (dolfinx/PETSc ADD_VALUES shape) */
 #define FA_ZERO_FIRST 0x2    /* FA_SCATTER only: zero A->data first (MatZeroEntries) */
 #define FA_DETERMINISTIC 0x4 /* FA_GATHER: bit-reproducible values, run to run (see below) */
-#define FA_CHECK_ERRORS 0x8  /* synchronise `stream` and return FA_E_PATTERN if a kernel found a (row, column)
-                                pair or a Dirichlet diagonal missing from the pattern (debugging) */
+#define FA_CHECK_ERRORS 0x8  /* validate the pattern and adjacency first (fa_check_pattern, when adj is given),
+                                then synchronise `stream` and return FA_E_PATTERN if a kernel found a (row,
+                                column) pair or a Dirichlet diagonal missing from the pattern (debugging) */
 /* Deterministic assembly (FA_DETERMINISTIC, or FA_PLAN_DETERMINISTIC in plan->cell_flags, which
  * fa_gather_rows honours too): the row gather adds every element contribution v of a row chunk as
  * the 64-bit integer round(v * 2^s) (s per chunk from a bound on its contributions, |v 2^s| < 2^50)
@@ -127,6 +128,9 @@ typedef struct {
                                 store); otherwise through the MFMA element kernel + block gather */
 #define FA_PLAN_DETERMINISTIC 0x2 /* set by the caller: assemblies with this plan (fa_assemble_matrix and
                                      fa_gather_rows) are deterministic, as with FA_DETERMINISTIC */
+#define FA_PLAN_ORDER_SEARCH 0x4  /* set by the caller before fa_plan_order: also run the alternating-path
+                                     moves of the bank-order search (fewer LDS bank conflicts, config E
+                                     ~0.5 % faster per assembly, plan ~10x slower: 1.7 -> 20 s) */
 
 /* Row-chunk plan for the gather kernel (host-computed once per pattern). */
 typedef struct {
@@ -162,6 +166,15 @@ int fa_build_adjacency(const fa_mesh* mesh, int64_t* ptr, int32_t* idx, void* st
  * (synchronises `stream` to read it); pass 2 fills indices [nblocks] sorted per row. */
 int fa_sparsity_count(const fa_mesh* mesh, const fa_adjacency* adj, int64_t* indptr, int64_t* nblocks, void* stream);
 int fa_sparsity_fill(const fa_mesh* mesh, const fa_adjacency* adj, const int64_t* indptr, int32_t* indices, void* stream);
+
+/* Validate a sparsity pattern and its adjacency on the device (synchronises `stream`): indptr[0] = 0,
+ * indptr monotone, indptr[nnodes] = nblocks; columns in [0, nnodes) and strictly increasing per row;
+ * adjacency ptr[nnodes] = ncells*nn, entries of node r sorted, unique and at dofmap positions holding
+ * r; every node of every cell present in the rows of the cell's nodes, and no other column (the
+ * pattern dolfinx create_matrix builds). FA_E_PATTERN with the failed checks in fa_last_error().
+ * The pattern and the adjacency come from rocPRIM sorts and scans (not code this library controls). */
+int fa_check_pattern(const fa_mesh* mesh, const fa_adjacency* adj, const int64_t* indptr, const int32_t* indices,
+                     int64_t nblocks, void* stream);
 
 /* Gather plan: row chunks whose blocks and adjacency fit the kernel's LDS budget.
  * row_start is a caller-owned device buffer of capacity nnodes+1; nchunks etc. returned

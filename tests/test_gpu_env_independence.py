@@ -45,8 +45,8 @@ a = fem.NeoHookean(V, E=1.0, nu=0.3, u=u)
 try:
     fem.assemble_matrix(a, plan=dict(order="steps"))
     out["neo_unordered"] = "assembled"
-except _lib.FemasmError as e:
-    out["neo_unordered"] = str(e).split(":")[0]
+except (ValueError, _lib.FemasmError) as e:  # refused up front (gather_plan) or by the library
+    out["neo_unordered"] = type(e).__name__ + ": " + str(e).split(":")[0]
 print(json.dumps(out))
 """
 

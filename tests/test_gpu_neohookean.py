@@ -127,9 +127,20 @@ def test_neohookean_gather_with_bcs(oracle, dev, ct, p, n):
 
 @pytest.mark.parametrize("order", ["steps", "none"])
 def test_neohookean_needs_positional_plan(oracle, dev, order):
-    """A plan without the positional order is refused (FA_E_ARG), never assembled another way."""
+    """A plan without the positional order is refused, never assembled another way: up front by
+    gather_plan (ValueError), and by the library itself (FA_E_ARG) when such a plan reaches
+    fa_assemble_matrix through the C ABI."""
+    import ctypes
+
     from femasm import _lib, fem
 
     m, V, a = _setup(oracle, -4, 2, (2, 2, 2), dev)
-    with pytest.raises(_lib.FemasmError, match="positional plan"):
+    with pytest.raises(ValueError, match="positional"):
         fem.assemble_matrix(a, plan=dict(order=order))
+    A = fem.create_matrix(a)
+    plan = fem.gather_plan(V, A, 0, _lib.FA_LINEAR_ELASTICITY, order=order)  # a linear-kind plan of that order
+    L = _lib.load()
+    rc = L.fa_assemble_matrix(ctypes.byref(V._fa_mesh()), ctypes.byref(fem._fa_form(a)), ctypes.byref(V._fa_adjacency()),
+                              ctypes.byref(plan), None, 1.0, ctypes.byref(A._fa_bsr(0)), _lib.FA_GATHER,
+                              _lib.stream_handle(dev))
+    assert rc == -1 and "positional plan" in L.fa_last_error().decode()

@@ -1,0 +1,150 @@
+"""Static check of the gfx950 store-data hazard in the SHIPPED library.
+
+Round 4 found a `buffer_store_dwordx4` whose data VGPRs the compiler rewrote two wait states after
+issue, before the store had read them: the stored values were torn. The library keeps every drain's
+store data live until the next barrier (`keep_vgprs`) and waits for the stores of the element /
+record kernels (`store_fence`). This checker disassembles the gfx950 code object inside
+libfemasm.so and reports every 12- or 16-byte vector-memory store (buffer / global / flat /
+scratch `_dwordx3` / `_dwordx4`) whose data VGPRs an instruction writes within WINDOW instructions
+after it (counted in wait states: one per instruction, k + 1 for `s_nop k`), with no
+`s_waitcnt vmcnt(0)` or `s_barrier` in between.
+
+Exempt (reported, not failed): scratch stores (the compiler's own register spills), rocPRIM's
+kernels (third-party, used by the sparsity build, whose pattern fa_check_pattern validates) and the
+HBM probe kernels `k_hbm_*` (measurement only; their stored values are never read).
+
+Usage: python tools/store_hazard.py [libfemasm.so] [--window N]
+"""
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+WINDOW = 16
+_STORE = re.compile(r"^(buffer|global|flat|scratch)_store_dwordx([34])$")
+_VREG = re.compile(r"^v(\d+)$|^v\[(\d+):(\d+)\]$")
+
+
+def disassemble(so: str) -> str:
+    with tempfile.TemporaryDirectory() as td:
+        fb, co = os.path.join(td, "fatbin.bin"), os.path.join(td, "co.o")
+        subprocess.run([f"{LLVM}/llvm-objcopy", "--dump-section", f".hip_fatbin={fb}", so, os.path.join(td, "x.so")],
+                       check=True, capture_output=True)
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fb}", f"--output={co}"],
+                       check=True, capture_output=True)
+        r = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", co], check=True, capture_output=True,
+                           text=True)
+        return r.stdout
+
+
+def vregs(tok: str):
+    m = _VREG.match(tok.strip())
+    if not m:
+        return None
+    if m.group(1) is not None:
+        v = int(m.group(1))
+        return set([v])
+    return set(range(int(m.group(2)), int(m.group(3)) + 1))
+
+
+def _operands(rest: str):
+    rest = rest.split("//")[0]
+    return [t.strip() for t in rest.split(",")] if rest.strip() else []
+
+
+def dest_vgprs(op: str, ops):
+    """VGPRs an instruction writes (its first operand for the forms that have a VGPR destination)."""
+    if not ops or op.startswith("s_"):
+        return set()
+    if op.startswith("ds_"):
+        has = op.startswith(("ds_read", "ds_load", "ds_swizzle", "ds_permute", "ds_bpermute", "ds_append",
+                             "ds_consume")) or "_rtn" in op
+        return (vregs(ops[0]) or set()) if has else set()
+    if op.startswith(("buffer_", "global_", "flat_", "scratch_")):
+        if "_store" in op:
+            return set()
+        if "_atomic" in op and not re.search(r"\b(sc0|glc)\b", " ".join(ops)):
+            return set()
+        return vregs(ops[0]) or set()
+    if op.startswith(("v_cmp", "v_readlane", "v_readfirstlane")):
+        return set()
+    return vregs(ops[0]) or set()
+
+
+def store_data(op: str, ops):
+    if op.startswith("buffer_"):
+        return vregs(ops[0])
+    return vregs(ops[1]) if len(ops) > 1 else None
+
+
+def check(text: str, window: int = WINDOW):
+    """[(function, store line, writer line, distance)] of every hazard site."""
+    sites = []
+    fn = None
+    insts = []  # (fn, op, ops, line)
+    for line in text.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+        if m:
+            fn = m.group(1)
+            continue
+        s = line.strip()
+        if not s or s.startswith(";") or fn is None or not line.startswith("\t"):
+            continue
+        parts = s.split(None, 1)
+        insts.append((fn, parts[0], _operands(parts[1]) if len(parts) > 1 else [], s.split("//")[0].strip()))
+    for i, (f, op, ops, ln) in enumerate(insts):
+        if not _STORE.match(op):
+            continue
+        data = store_data(op, ops)
+        if not data:
+            continue
+        ws = 0
+        for d in range(1, 4 * window + 1):
+            if i + d >= len(insts) or insts[i + d][0] != f:
+                break
+            f2, op2, ops2, ln2 = insts[i + d]
+            if op2 == "s_barrier" or op2 == "s_endpgm" or (op2 == "s_waitcnt" and "vmcnt(0)" in " ".join(ops2)):
+                break
+            if dest_vgprs(op2, ops2) & data:
+                sites.append((f, ln, ln2, ws + 1))
+                break
+            ws += int(ops2[0], 0) + 1 if op2 == "s_nop" and ops2 else 1
+            if ws >= window:
+                break
+    return sites
+
+
+def exempt(fn: str, store: str) -> bool:
+    return store.startswith("scratch_") or "rocprim" in fn or fn.startswith("_Z11k_hbm_") or "k_hbm_" in fn
+
+
+def product_sites(so: str, window: int = WINDOW):
+    """The hazard sites that are not exempt (the CPU / GPU tests require none)."""
+    return [s for s in check(disassemble(so), window) if not exempt(s[0], s[1])]
+
+
+def demangle(names):
+    r = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True)
+    return r.stdout.splitlines()
+
+
+if __name__ == "__main__":
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    so = args[0] if args else "fem-libraries_amd/femasm/lib/libfemasm.so"
+    w = WINDOW
+    if "--window" in sys.argv:
+        w = int(sys.argv[sys.argv.index("--window") + 1])
+    sites = check(disassemble(so), w)
+    names = demangle([s[0] for s in sites]) if sites else []
+    bad = 0
+    for (f, ln, ln2, d), n in zip(sites, names):
+        ex = exempt(f, ln)
+        bad += not ex
+        print(f"{'exempt' if ex else 'SITE  '} {d:3d}  {n[:90]}\n       {ln}\n       {ln2}")
+    print(f"{len(sites)} site(s) within {w} wait states, {bad} not exempt")
+    sys.exit(1 if bad else 0)
