@@ -294,6 +294,69 @@ def cpu_baseline(sample_n: int, reps: int):
     return m.num_cells / t / 1e6, m.num_cells, t
 
 
+def time_steps(step, steps: int, warmup: int, dev, dist=None):
+    """W untimed steps, then K steps bracketed by a barrier + synchronize on both sides; returns the
+    wall seconds of the K steps and the mean launch time (HIP events on the launch stream, ms)."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(steps):
+        evs[k][0].record(stream)
+        step()
+        evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    return time.perf_counter() - t_start, float(np.mean([s.elapsed_time(e) for s, e in evs]))
+
+
+def eneo_block(dev, steps: int, warmup: int) -> dict:
+    """Config E as BASELINE.json states its physics: the neo-Hookean AD tangent on the same 50.2 M-cell
+    P2 mesh, timed in this process after the linear problem is freed (secondary block of the default
+    line: the driver's clock covers it). FP64-VALU-bound: its roof is the executed FP64 flops (PMC
+    record of this build, profiles/traffic.json) over the 78.6 TF/s FP64 peak; no MFMA is issued."""
+    from femasm import fem
+
+    cfg = CONFIGS["Eneo"]
+    n = cfg["n"]
+    t0 = time.time()
+    m, V, a, bcs = build_problem(n, dev, cfg=cfg)
+    A = fem.create_matrix(a)
+    fem.gather_plan(V, A, 0, a.kind)
+    torch.cuda.synchronize()
+    setup = time.time() - t0
+    elapsed, launch_ms = time_steps(lambda: fem.assemble_matrix(a, bcs=bcs, A=A), steps, warmup, dev)
+    ms = elapsed / steps * 1e3
+    comp = compulsory_bytes(V, A, m.num_cells, True, state=True)
+    trec, tsrc = measured_traffic("Eneo", n, 1)
+    flops = None if trec is None else trec.get("fp64_flops")
+    tf = None if flops is None else flops / (launch_ms * 1e-3) / 1e12
+    out = {
+        "workload": f"config E physics: {cfg['label']}, {m.num_cells} cells, E=E_range[cell%200], nu=0.3, "
+                    f"x=0 clamped / x=1 prescribed, BSR(3) global matrix",
+        "ms_per_step": round(ms, 4), "value": round(m.num_cells / (ms * 1e-3) / 1e6, 3), "unit": "Melements/s",
+        "steps": steps, "warmup": warmup, "launch_ms": round(launch_ms, 4), "setup_s": round(setup, 2),
+        "bound": "fp64_valu",
+        "fp64_executed": None if flops is None else {
+            "flops_per_launch": flops, "TFLOPs": round(tf, 3), "peak_TFLOPs": FP64_PEAK_TFLOPS,
+            "frac": round(tf / FP64_PEAK_TFLOPS, 4)},
+        "hbm": {"algorithmic_bytes": comp["total"],
+                "achieved_GBps": round(comp["total"] / (launch_ms * 1e-3) / 1e9, 1),
+                "frac": round(comp["total"] / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)},
+        "traffic": None if trec is None else round(trec["bytes"] / 1e9, 3),
+        "traffic_source": tsrc,
+    }
+    del A, a, V, m, bcs
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -313,6 +376,8 @@ def main():
                     help="N > 1: RCCL interface exchange (default) or the communication-free redundant "
                          "ghost layer (SURVEY §8(e) alternative)")
     ap.add_argument("--no-hbm-probe", action="store_true", help="skip the measured-HBM-peak stream probe")
+    ap.add_argument("--no-eneo", action="store_true",
+                    help="config E at N = 1: skip the secondary neo-Hookean (config E physics) block")
     ap.add_argument("--cpu-all-affinity", type=int, default=1,
                     help="1: also time the CPU baseline with one process per affinity core (beyond the CPU share)")
     ap.add_argument("--cpu-cores", type=int, default=0,
@@ -405,26 +470,8 @@ def main():
     log(f"[bench] setup {setup_s:.1f}s (pattern {t_pattern:.1f}s, plan {t_plan:.1f}s): {ncells_local} cells "
         f"on rank {rank}")
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    # per-launch kernel durations, HIP events on the launch stream (torch's current stream)
-    stream = torch.cuda.current_stream(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for k in range(args.steps):
-        evs[k][0].record(stream)
-        step()
-        evs[k][1].record(stream)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    launch_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    # per-launch kernel durations: HIP events on the launch stream (torch's current stream)
+    elapsed, launch_ms = time_steps(step, args.steps, args.warmup, dev, dist)
     if dist is not None:
         t = torch.tensor([elapsed, launch_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -474,6 +521,17 @@ def main():
     # the FP64 roof applies only with a PMC flop count of this very build; otherwise the line
     # reports the HBM roof (F_e is a model of a contraction this kernel does not run)
     compute_bound = compute_bound and tflops_exec is not None
+
+    eneo = None
+    if world == 1 and args.config == "E" and not args.no_eneo and args.method == "gather" and not args.deterministic \
+            and (args.n or cfg["n"]) == CONFIGS["Eneo"]["n"]:
+        del step, V_loc, A_loc, A, a, V, m, bcs  # the linear problem's ~150 GB
+        torch.cuda.empty_cache()
+        try:
+            eneo = eneo_block(dev, args.steps, args.warmup)
+        except Exception as e:  # a secondary block: recorded, never fails the headline line
+            eneo = {"error": f"{type(e).__name__}: {e}"}
+            log(f"[bench] E-neo block failed: {e}")
 
     cpu = None
     if cpu_ctx is not None:
@@ -548,7 +606,7 @@ def main():
                                        f"above its slab (redundant ghost layer) so its owned rows are complete")
                        if world > 1 else "single GPU"},
             # per GPU (rank 0 / slowest rank): achieved = algorithmic bytes of the assembly / launch time
-            "roofline": {"bound": "mfma" if compute_bound else "hbm",
+            "roofline": {"bound": "fp64_valu" if compute_bound else "hbm",
                          "achieved": round(tflops_exec, 3) if compute_bound else round(achieved, 1),
                          "achieved_source": "PMC SQ_INSTS_VALU_FLOPS_FP64 of this build (executed FP64 flops, FP64 "
                                             "VALU; no MFMA in this kernel) / launch time" if compute_bound
@@ -584,6 +642,7 @@ def main():
                              "what": "SURVEY §8(d) B_e: bytes a reference-shaped element scatter moves "
                                      "(read + write of every element-matrix value); not moved by the gather"}},
             "cpu_baseline": cpu,
+            "eneo": eneo,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -2248,6 +2248,42 @@ __device__ __forceinline__ void chunk_drain(double* acc, int h, int nv, double* 
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rs,
                                         (tid == (jt % NT) && tail_half && !(jt == 0 && h)) ? 8 * (h + nv - 1) : OOB, 0, AUX);
 }
+// k_gather_lin's drain as a function (k_gather_neo, round 5): after the items barrier, every value of
+// the chunk is exchanged with zero into registers (ds_wrxchg_rtn_b64 at raised wave priority: the
+// exchanges issue ahead of other workgroups' atomics), then stored with SW 16-B buffer stores per lane
+// plus the unpaired head / tail value (lanes without one store past the descriptor's range: dropped).
+// The caller's next barrier, then keep_vgprs(v, hv, tv), as in k_gather_lin.
+template <int SW, int NT = 256>
+__device__ __forceinline__ void xchg_drain(double* acc, int h, int nv, double* out, int tid, fa_dv2 (&v)[SW],
+                                           double& hv, double& tv) {
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  typedef unsigned v2u __attribute__((ext_vector_type(2)));
+  const int np = (nv - h) >> 1;
+  const bool tail = ((nv - h) & 1) != 0;
+  hv = 0.0;
+  tv = 0.0;
+  __builtin_amdgcn_s_setprio(3);
+  auto xchg = [&](double* p) -> double { return __hip_atomic_exchange(p, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+#pragma unroll
+  for (int u = 0; u < SW; ++u) {
+    v[u] = fa_dv2{0.0, 0.0};
+    if (tid + NT * u < np) {
+      double* pp = acc + 2 * (h + tid + NT * u);
+      v[u] = fa_dv2{xchg(pp), xchg(pp + 1)};
+    }
+  }
+  if (tid == 0 && h) hv = xchg(acc + 1);
+  if (tid == 1 && tail) tv = xchg(acc + nv - 1 + h);
+  __builtin_amdgcn_s_setprio(0);
+  constexpr int OOB = 0x40000000, NTS = 2;  // nt
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(out, 0, 8 * nv, 0x00020000);
+  const int base = 8 * h + 16 * tid, lim = np - tid;
+#pragma unroll
+  for (int u = 0; u < SW; ++u)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v[u]), rv, NT * u < lim ? base : OOB, 16 * NT * u, NTS);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, hv), rv, (tid == 0 && h) ? 0 : OOB, 0, NTS);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rv, (tid == 1 && tail) ? 8 * (nv - 1) : OOB, 0, NTS);
+}
 constexpr int FA_LIN_FUSE = 1;  // P1 simplices (fa_assemble_matrix): records formed inside k_gather_lin
 // 2^e for a normal exponent (|e| <= 1022), from its bits (no FP64 op: uniform e stays scalar)
 __device__ __forceinline__ double pow2(int e) { return __hiloint2double((e + 1023) << 20, 0); }
@@ -2479,7 +2515,24 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
     const int h = (int)(off & 1);
     const int nb = d0.nb;
     const bool valid = jit < d0.na;
-    {
+    // The LDS adds are issued by every lane (no branch): a lane without an item of this chunk (or, on
+    // a broken pattern, with a slot past the chunk) adds zeros -- its record's s Ji zeroed -- to an
+    // in-chunk slot of its own. Behind a branch the compiler could not count the outstanding LDS
+    // operations and waited for each block's adds to complete (lgkmcnt(0)) before the next block's
+    // prefetched table word.
+    // (P2 / table blocks: config E 35.2 vs 36.0 ms. P1 simplices keep the branch: C 1.10 vs 1.11 ms,
+    // their items are four table-free blocks)
+    constexpr bool UNC = !P1G;
+    int smax = 0;
+#pragma unroll
+    for (int bb = 0; bb < NBG; ++bb) smax = max(smax, (int)((cur.sl[bb / 2] >> (16 * (bb % 2))) & 1023u));
+    bad |= valid && smax >= d0.nb;
+    const bool eff = valid && smax < d0.nb;
+    if constexpr (UNC) {
+#pragma unroll
+      for (int kk = 0; kk < BS2; ++kk) cur.r[kk] = eff ? cur.r[kk] : 0.0;
+    }
+    if (__any(eff)) {  // wave-uniform: a wave without items (a short chunk's last waves) skips them
       const int aloc = pf0 % NN;
       // the row's packed blocks: one ds_read_b64 per block (nine for a table of doubles)
       const uint64_t* Ah0 = tab + aloc * NN;
@@ -2585,9 +2638,9 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
             for (int kk = 0; kk < GD; ++kk)
               if (((rowm >> i) | (colm >> kk)) & 1u) G[i][kk] = 0.0;
         }
-        bad |= valid && s >= nb;
-        if (valid && s < nb) {
-          double* ap = acc + h + s * BS2;
+        if (UNC || eff) {
+          const int sd = eff ? s : ((tid & 63) < nb ? (tid & 63) : 0);  // (zeros) distinct slots
+          double* ap = acc + h + sd * BS2;
           if constexpr (FIX) {
 #pragma unroll
             for (int i = 0; i < GD; ++i)
@@ -2869,8 +2922,8 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
                 "k_gather_neo: affine simplices");
   typedef double dv2 __attribute__((ext_vector_type(2)));
   __shared__ __attribute__((aligned(16))) double acc[2 * NP2];
-  __shared__ double s_phi[NN * NQ * GD];  // [b][q][k]: a column's gradients at every point, contiguous
-  __shared__ double s_T[NN * NN * NT];    // [a][b][t]
+  __shared__ __attribute__((aligned(16))) double s_phi[NN * NQ * GD];  // [b][q][k]: a column's gradients at every point, contiguous
+  __shared__ __attribute__((aligned(16))) double s_T[NN * NN * NT];    // [a][b][t]
   dv2* acc2 = reinterpret_cast<dv2*>(acc);
   const int tid = threadIdx.x;
   // chunk schedule of k_gather_lin (round 5): the resident grid pulls chunks from 8 per-XCD counters,
@@ -2971,7 +3024,6 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
   int bad = 0;
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the prologue's loads (see k_gather_lin)
   __syncthreads();                     // tables and accumulator staged
-  typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
   for (int k = 0; d0.nb >= 0; ++k) {
     unsigned int rn = 0u;  // the id of chunk k + AHEAD (atomicInc: see k_gather_lin)
     if (tid == 0) rn = atomicInc(lctr, 0xFFFFFFFFu);
@@ -2984,7 +3036,19 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
     {
       const int aloc = pf0 % NN;
       const uint32_t rowm = (cur.mask >> (aloc * GD)) & ((1u << GD) - 1);
-      const double sc = cur.hd[NT];
+      // The LDS adds are issued by every lane (no branch): a lane without an item of this chunk (or,
+      // on a broken pattern, with a slot past the chunk) adds zeros to an in-chunk slot of its own.
+      // Behind a branch the compiler could not count the outstanding LDS operations and waited for
+      // each block's adds to complete (lgkmcnt(0)) before the next block's prefetched table values.
+      int smax = 0;
+#pragma unroll
+      for (int bb = 0; bb < NBG; ++bb) smax = max(smax, (int)((cur.sl[bb / 2] >> (16 * (bb % 2))) & 1023u));
+      bad |= valid && smax >= nb;
+      const bool eff = valid && smax < nb;
+      if (__any(eff)) {  // wave-uniform: a wave without items skips them
+      const double sc = eff ? cur.hd[NT] : 0.0;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) cur.hd[t] = eff ? cur.hd[t] : 0.0;
       // per point: U = M_q dphi_a, W = s_c U, Z = rho_q U
       double W[NQL][GD], Z[NQL][GD];
 #pragma unroll
@@ -2999,16 +3063,33 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
 #pragma unroll
           for (int kk = 1; kk < GD; ++kk) u = fma(cur.pt[ql][i * GD + kk], pa[kk], u);
           W[ql][i] = sc * u;
-          Z[ql][i] = cur.pt[ql][BS2] * u;
+          Z[ql][i] = (eff ? cur.pt[ql][BS2] : 0.0) * u;
         }
       }
-      lds_vdouble* Ta = (lds_vdouble*)(s_T + aloc * NN * NT);
+      // the column's table values (its gradients at every point, its mu-term block) of block bb + 1
+      // are read into registers while block bb computes: the reads' LDS latency is not exposed per
+      // point (round 4 read them through a volatile pointer right before each use: 3-4 dependent
+      // waits per point, 5 blocks per item)
+      const double* Ta = s_T + aloc * NN * NT;
+      auto col_of = [&](int bb) -> uint32_t { return (cur.sl[bb / 2] >> (16 * (bb % 2))) & 0xFFFFu; };
+      // (the mu-term block is read at the top of its own block: it is needed last)
+      struct Col { double ph[NQL * GD]; };
+      auto load_col = [&](int b, Col& c) {
+#pragma unroll
+        for (int u = 0; u < NQL * GD; ++u) c.ph[u] = s_phi[b * NQ * GD + u];
+      };
+      Col cn;
+      load_col((int)(col_of(0) >> 10), cn);
 #pragma unroll
       for (int bb = 0; bb < NBG; ++bb) {
-        const uint32_t slv = (cur.sl[bb / 2] >> (16 * (bb % 2))) & 0xFFFFu;
+        const uint32_t slv = col_of(bb);
         const int s = (int)(slv & 1023u);
         const int b = (int)(slv >> 10);
-        lds_vdouble* pb = (lds_vdouble*)(s_phi + b * NQ * GD);
+        const Col cc = cn;
+        double tt[NT];
+#pragma unroll
+        for (int u = 0; u < NT; ++u) tt[u] = Ta[b * NT + u];
+        if (bb + 1 < NBG) load_col((int)(col_of(bb + 1) >> 10), cn);
         double K[GD][GD];
 #pragma unroll
         for (int i = 0; i < GD; ++i)
@@ -3016,14 +3097,12 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
           for (int kk = 0; kk < GD; ++kk) K[i][kk] = 0.0;
 #pragma unroll
         for (int ql = 0; ql < NQL; ++ql) {
-          double pbq[GD], V[GD];
-#pragma unroll
-          for (int kk = 0; kk < GD; ++kk) pbq[kk] = pb[ql * GD + kk];
+          double V[GD];
 #pragma unroll
           for (int i = 0; i < GD; ++i) {
-            double v = cur.pt[ql][i * GD] * pbq[0];
+            double v = cur.pt[ql][i * GD] * cc.ph[ql * GD];
 #pragma unroll
-            for (int kk = 1; kk < GD; ++kk) v = fma(cur.pt[ql][i * GD + kk], pbq[kk], v);
+            for (int kk = 1; kk < GD; ++kk) v = fma(cur.pt[ql][i * GD + kk], cc.ph[ql * GD + kk], v);
             V[i] = v;
           }
 #pragma unroll
@@ -3034,7 +3113,7 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
         {
           double dot = 0.0;
 #pragma unroll
-          for (int t = 0; t < NT; ++t) dot = fma(cur.hd[t], Ta[b * NT + t], dot);
+          for (int t = 0; t < NT; ++t) dot = fma(cur.hd[t], tt[t], dot);
 #pragma unroll
           for (int i = 0; i < GD; ++i) K[i][i] += dot;
         }
@@ -3046,14 +3125,15 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
             for (int kk = 0; kk < GD; ++kk)
               if (((rowm >> i) | (colm >> kk)) & 1u) K[i][kk] = 0.0;
         }
-        bad |= valid && s >= nb;
-        if (valid && s < nb) {
-          double* ap = acc + h + s * BS2;
+        const int se = eff ? s : ((tid & 63) < nb ? (tid & 63) : 0);  // (zeros) distinct slots
+        {
+          double* ap = acc + h + se * BS2;
 #pragma unroll
           for (int i = 0; i < GD; ++i)
 #pragma unroll
             for (int kk = 0; kk < GD; ++kk) atomicAdd(ap + i * GD + kk, K[i][kk]);
         }
+      }
       }
     }
     // chunk k+1's records / slots / masks: the item registers are dead here, and these loads are
@@ -3062,7 +3142,7 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
     __syncthreads();  // B1: the chunk is accumulated
     fa_dv2 dv[SW];
     double dh, dt;
-    chunk_drain<SW, NTH>(acc, h, nb * BS2, P.A.data + off, tid, dv, dh, dt);
+    xchg_drain<SW, NTH>(acc, h, nb * BS2, P.A.data + off, tid, dv, dh, dt);
     __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics
     keep_vgprs(dv, dh, dt);
     // chunk k + AHEAD's id, read at iteration k + AHEAD - LOOK (after later barriers)

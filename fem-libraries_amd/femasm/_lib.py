@@ -135,7 +135,11 @@ def load(path: str | None = None):
             "or __graft_entry__.build(); femasm has no CPU fallback")
     L = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(L, name)
+        fn = getattr(L, name, None)
+        if fn is None:
+            if os.path.abspath(path) == os.path.abspath(LIB_PATH):
+                raise FemasmError(f"{path} does not export {name}: rebuild it (make -C {CSRC})")
+            continue  # an older measurement build (FEMASM_LIB, A/B runs): entry points it lacks stay unbound
         fn.restype = res
         fn.argtypes = args
     _lib = L

@@ -13,7 +13,7 @@ for c in ${CFGS:-E Eneo}; do
   i=0; mkdir -p gpurun_out/diag_$c
   for p in "${passes[@]}"; do
     timeout -s KILL 300 rocprofv3 --kernel-include-regex 'k_gather' --pmc $p -d gpurun_out/diag_$c/pass$i -o run --output-format csv -- \
-      python bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/diag_$c/pass$i.log 2>&1 || { echo "$c pass $i failed"; tail -3 gpurun_out/diag_$c/pass$i.log; exit 1; }
+      python bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-hbm-probe --no-eneo > gpurun_out/diag_$c/pass$i.log 2>&1 || { echo "$c pass $i failed"; tail -3 gpurun_out/diag_$c/pass$i.log; exit 1; }
     i=$((i+1))
   done
   python tools/pmc_summary.py gpurun_out/diag_$c > gpurun_out/diag_$c.txt || exit 1

@@ -62,18 +62,47 @@ V = {
         "  if (blockIdx.x == 0 && threadIdx.x == 0) printf(\"neo_timing %llu %llu %llu %llu %llu %llu %llu\\n\", tmo[0], tmo[1], tmo[2], tmo[3], tmo[4], tmo[5], tmo[6]);\n"
         "  unsigned long long t_prev = __builtin_amdgcn_s_memtime(), r_prev = __builtin_amdgcn_s_memrealtime();\n"
         "#define FN_T(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if ((threadIdx.x & 63) == 0) atomicAdd(&s_tm[threadIdx.x >> 6][i], t_ - t_prev); t_prev = t_; }\n"), (
-        "  for (int64_t k = 0; k < cnt; ++k) {\n    const int32_t pf2 = load_entry(d2);",
-        "  for (int64_t k = 0; k < cnt; ++k) {\n    FN_T(4);\n"
+        "  for (int k = 0; d0.nb >= 0; ++k) {\n    unsigned int rn = 0u;",
+        "  for (int k = 0; d0.nb >= 0; ++k) {\n    FN_T(4);\n"
         "    { const unsigned long long r_ = __builtin_amdgcn_s_memrealtime(); if ((threadIdx.x & 63) == 0) { atomicAdd(&s_tm[threadIdx.x >> 6][5], 1ull); atomicAdd(&s_tm[threadIdx.x >> 6][6], r_ - r_prev); } r_prev = r_; }\n"
-        "    const int32_t pf2 = load_entry(d2);"), (
+        "    unsigned int rn = 0u;"), (
         "    // chunk k+1's records / slots / masks: the item registers are dead here, and these loads are\n",
         "    FN_T(0);\n    // chunk k+1's records / slots / masks: the item registers are dead here, and these loads are\n"), (
         "    __syncthreads();  // B1: the chunk is accumulated\n    fa_dv2 dv[SW];",
         "    __syncthreads();  // B1: the chunk is accumulated\n    FN_T(1);\n    fa_dv2 dv[SW];"), (
-        "    __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics\n    keep_vgprs(dv, dh, dt);\n    d0 = d1;",
-        "    FN_T(2);\n    __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics\n    keep_vgprs(dv, dh, dt);\n    FN_T(3);\n    d0 = d1;"), (
+        "    __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics\n    keep_vgprs(dv, dh, dt);\n    // chunk k + AHEAD's id",
+        "    FN_T(2);\n    __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics\n    keep_vgprs(dv, dh, dt);\n    FN_T(3);\n    // chunk k + AHEAD's id"), (
         "  if (bad) atomicOr(P.err, 1);\n}\n\n// ------------------------------------------------------------------------------ block-owner gather",
         "  if (bad) atomicOr(P.err, 1);\n  __syncthreads();\n  if (threadIdx.x < 7) { unsigned long long t = 0; for (int w = 0; w < 4; ++w) t += s_tm[w][threadIdx.x]; atomicAdd(tmo + threadIdx.x, t); }\n}\n\n// ------------------------------------------------------------------------------ block-owner gather")],
+    # k_gather_neo ablations (timing only, wrong matrices; round 5): the phi-table reads replaced by a
+    # per-lane register value, the mu-term table reads likewise, no LDS accumulate, no chunk stores
+    "neo_nophi": [(
+        "          for (int kk = 0; kk < GD; ++kk) pbq[kk] = pb[ql * GD + kk];",
+        "          for (int kk = 0; kk < GD; ++kk) pbq[kk] = fake_phi + (double)(ql * GD + kk);"), (
+        "  for (int t = tid; t < NP2; t += NTH) acc2[t] = dv2{0.0, 0.0};\n\n  const int32_t* __restrict__ eadj = P.eadj;",
+        "  for (int t = tid; t < NP2; t += NTH) acc2[t] = dv2{0.0, 0.0};\n  const double fake_phi = P.tab[tid % 8];\n  const int32_t* __restrict__ eadj = P.eadj;")],
+    "neo_noT": [(
+        "          for (int t = 0; t < NT; ++t) dot = fma(cur.hd[t], Ta[b * NT + t], dot);",
+        "          for (int t = 0; t < NT; ++t) dot = fma(cur.hd[t], fake_phi + (double)t, dot);"), (
+        "  for (int t = tid; t < NP2; t += NTH) acc2[t] = dv2{0.0, 0.0};\n\n  const int32_t* __restrict__ eadj = P.eadj;",
+        "  for (int t = tid; t < NP2; t += NTH) acc2[t] = dv2{0.0, 0.0};\n  const double fake_phi = P.tab[tid % 8];\n  const int32_t* __restrict__ eadj = P.eadj;")],
+    "neo_noadd": [(
+        "            for (int kk = 0; kk < GD; ++kk) atomicAdd(ap + i * GD + kk, K[i][kk]);\n        }\n      }\n    }\n    // chunk k+1's records",
+        "            for (int kk = 0; kk < GD; ++kk) if (K[i][kk] == 1.2345e-300) ap[i * GD + kk] = 1.0;\n        }\n      }\n    }\n    // chunk k+1's records")],
+    "neo_nostore": [(
+        "    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v[u]), rs, full ? 16 * j : OOB, 0, AUX);",
+        "    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v[u]), rs, OOB + 0 * full, 0, AUX);")],
+    # (round 5) the item record loads: none (points faked from the cell index) / half (points 2, 3 copied
+    # from points 0, 1)
+    "neo_norec": [(
+        "        const dv2 v = pp[k];\n        it.pt[ql][2 * k] = v.x;",
+        "        const dv2 v = dv2{(double)c * 1e-9 + k, (double)ql + 0.5};\n        it.pt[ql][2 * k] = v.x;")],
+    "neo_halfrec": [(
+        "        const dv2 v = pp[k];\n        it.pt[ql][2 * k] = v.x;",
+        "        const dv2 v = ql < 2 ? pp[k] : dv2{it.pt[ql - 2][2 * k], it.pt[ql - 2][2 * k + 1]};\n        it.pt[ql][2 * k] = v.x;")],
+    "neo_nostore2": [(
+        "    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v[u]), rv, NT * u < lim ? base : OOB, 16 * NT * u, NTS);\n  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, hv), rv, (tid == 0 && h) ? 0 : OOB, 0, NTS);\n  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rv, (tid == 1 && tail) ? 8 * (nv - 1) : OOB, 0, NTS);\n}",
+        "    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v[u]), rv, OOB + 0 * lim, 16 * NT * u, NTS);\n  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, hv), rv, OOB, 0, NTS);\n  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rv, OOB + 0 * tail, 0, NTS);\n}")],
 }
 
 
