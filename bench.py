@@ -10,8 +10,11 @@ are resident in HBM before timing.
 Workload: config E's mesh — unit cube, 203^3 cubes x 6 Kuhn tetrahedra = 50,192,562 P2 cells,
 202,257,429 dofs — with the linear-elasticity J (d = 0), nu = 0.3, E = E_range[cell % 200]
 (libc srand(6575) table), x=0 clamped and x=1 prescribed. N > 1 ranks (one per GPU) shard the
-cube into z-slabs (strong scaling: fixed total mesh); shared slab-interface rows are summed with
-an RCCL exchange between slab neighbours (femasm.parallel).
+cube into z-slabs (strong scaling: fixed total mesh); by default each rank also assembles the cell
+layer above its slab (ghost mode: its owned rows complete with no data-path collective), or, with
+--slab-mode exchange, shared slab-interface rows are summed with an RCCL exchange between slab
+neighbours (femasm.parallel). At N = 1 with config E the line also carries an "eneo" block: the
+neo-Hookean AD tangent (config E's physics) timed on the same mesh in the same process.
 
 Prints ONE JSON line (rank 0).
 """
@@ -372,9 +375,12 @@ def main():
     ap.add_argument("--cpu-reps", type=int, default=7)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true", help="N > 1: exchange after all rows (no overlap)")
-    ap.add_argument("--slab-mode", default="exchange", choices=["exchange", "ghost"],
-                    help="N > 1: RCCL interface exchange (default) or the communication-free redundant "
-                         "ghost layer (SURVEY §8(e) alternative)")
+    ap.add_argument("--slab-mode", default="ghost", choices=["exchange", "ghost"],
+                    help="N > 1: the communication-free redundant ghost layer (default, SURVEY §8(e) alternative) "
+                         "or the RCCL interface exchange. Ghost is the default since round 5: on one GPU a transfer "
+                         "paced to an xGMI link beside the interior rows was starved of CUs by the persistent gather "
+                         "(rank 3 of 8: interior + transfer 6.24 ms against a 4.78 ms ghost-mode slab; "
+                         "profiles/r5/overlap_*.json, DESIGN.md §7)")
     ap.add_argument("--no-hbm-probe", action="store_true", help="skip the measured-HBM-peak stream probe")
     ap.add_argument("--no-eneo", action="store_true",
                     help="config E at N = 1: skip the secondary neo-Hookean (config E physics) block")

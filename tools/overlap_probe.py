@@ -7,7 +7,10 @@ boundary's transfer (the interface suffix the rank sends, ~0.28 GB) runs on a se
 same slab's ghost-mode assembly (its layers + the layer above, no exchange). HIP events on the
 stream each kernel runs on. Writes one JSON line.
 
-usage: python tools/overlap_probe.py [--n 203] [--rank 3] [--world 8] [--reps 10]
+Round 5: also the same transfer PACED to one xGMI link direction (--link-GBps, --pieces copies separated
+by spin kernels), whose duration matches the real exchange's, beside the interior rows.
+
+usage: python tools/overlap_probe.py [--n 203] [--rank 3] [--world 8] [--reps 10] [--link-GBps 70]
 """
 import argparse
 import json
@@ -42,6 +45,9 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--form", default="linear")
+    ap.add_argument("--link-GBps", dest="link_GBps", type=float, default=70.0,
+                    help="paced transfer rate: one xGMI link direction (~153 GB/s per link both ways; ~64-76 GB/s one way)")
+    ap.add_argument("--pieces", type=int, default=64)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     out = {"n": args.n, "rank": args.rank, "world": args.world, "form": args.form}
@@ -85,6 +91,47 @@ def main():
         cur.wait_stream(side)
     out["interior_with_copy_ms"], out["interior_with_copy_min_ms"] = timed(interior_with_copy, args.reps, cur)
     out["overlap_cost_ms"] = out["interior_with_copy_ms"] - out["interior_alone_ms"]
+
+    # round 5: the transfer paced to an xGMI link's rate -- the same bytes in
+    # `--pieces` device copies on the side stream, separated by spin kernels (torch.cuda._sleep) so
+    # that the whole transfer lasts as long as `--link-GBps` would take, overlapping the interior rows
+    cyc = 1 << 20
+    sleep_ms, _ = timed(lambda: torch.cuda._sleep(cyc), 5, cur)
+    cyc_per_ms = cyc / max(sleep_ms, 1e-6)
+    target_ms = nbytes / (args.link_GBps * 1e6)
+    piece = (src.numel() + args.pieces - 1) // args.pieces
+    gap = max(int(cyc_per_ms * target_ms / args.pieces), 1)
+
+    def paced():
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for k in range(args.pieces):
+                dst[k * piece:(k + 1) * piece].copy_(src[k * piece:(k + 1) * piece])
+                torch.cuda._sleep(gap)
+    out["paced_target_ms"] = target_ms
+    out["paced_alone_ms"], _ = timed(lambda: (paced(), cur.wait_stream(side)), args.reps, cur)
+
+    def interior_with_paced():
+        paced()
+        sg.rows(inner)
+        cur.wait_stream(side)
+    out["interior_with_paced_ms"], out["interior_with_paced_min_ms"] = timed(interior_with_paced, args.reps, cur)
+
+    def interior_then_wait_paced():  # the interior's own time while the paced transfer runs beside it
+        paced()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(cur)
+        sg.rows(inner)
+        e1.record(cur)
+        cur.wait_stream(side)
+        return e0, e1
+    ts = []
+    for _ in range(args.reps):
+        e0, e1 = interior_then_wait_paced()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    out["interior_beside_paced_ms"] = statistics.median(ts)
+    out["paced_pieces"], out["link_GBps"] = args.pieces, args.link_GBps
     del prob, sg
     torch.cuda.empty_cache()
     ghost = SlabProblem(args.n, args.rank, args.world, dev, groups=[None] * (args.world - 1), form=args.form,
