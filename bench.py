@@ -382,6 +382,8 @@ def main():
                          "(rank 3 of 8: interior + transfer 6.24 ms against a 4.78 ms ghost-mode slab; "
                          "profiles/r5/overlap_*.json, DESIGN.md §7)")
     ap.add_argument("--no-hbm-probe", action="store_true", help="skip the measured-HBM-peak stream probe")
+    ap.add_argument("--plan-search", action="store_true",
+                    help="plan the LDS order with the alternating-path search (FA_PLAN_ORDER_SEARCH: ~10x plan time)")
     ap.add_argument("--no-eneo", action="store_true",
                     help="config E at N = 1: skip the secondary neo-Hookean (config E physics) block")
     ap.add_argument("--cpu-all-affinity", type=int, default=1,
@@ -462,14 +464,16 @@ def main():
         torch.cuda.synchronize()
         t2 = time.time()
         for part in range(len(A.parts)):
-            fem.gather_plan(V, A, part, a.kind, deterministic=args.deterministic)  # chunks, slot map, LDS order
+            fem.gather_plan(V, A, part, a.kind, deterministic=args.deterministic,  # chunks, slot map, LDS order
+                            **({"search": True} if args.plan_search else {}))
         torch.cuda.synchronize()
         t_pattern, t_plan = t2 - t1, time.time() - t2
         ncells_local = m.num_cells
         V_loc, A_loc, with_bc = V, A, True
 
         def step():
-            fem.assemble_matrix(a, bcs=bcs, A=A, method=args.method, deterministic=args.deterministic)
+            fem.assemble_matrix(a, bcs=bcs, A=A, method=args.method, deterministic=args.deterministic,
+                                plan={"search": True} if args.plan_search else None)
 
     torch.cuda.synchronize()
     setup_s = time.time() - t0

@@ -3753,12 +3753,25 @@ extern "C" int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const
 // times per Newton solve)
 constexpr int kKempeRounds = 4;
 constexpr int kKempeLen = 6;
+// The search's per-thread state (residues, picks, counts, step maxima) sits in LDS, one slice per
+// thread of a 64-thread workgroup (round 5; in scratch it made the search with the alternating-path
+// moves a 19.6-s launch on config E).
+constexpr int kOrderThreads = 64;
 template <int NN, int NSPLIT>
-__global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64_t* __restrict__ indptr,
-                              const int64_t* __restrict__ adj_ptr, int64_t nchunks, int groups_per_chunk,
-                              uint16_t* __restrict__ slots, const uint16_t* __restrict__ src,
-                              const uint16_t* __restrict__ eperm, int rounds) {
+__global__ __launch_bounds__(kOrderThreads) void k_order_slots(const int64_t* __restrict__ row_start,
+                                                                const int64_t* __restrict__ indptr,
+                                                                const int64_t* __restrict__ adj_ptr, int64_t nchunks,
+                                                                int groups_per_chunk, uint16_t* __restrict__ slots,
+                                                                const uint16_t* __restrict__ src,
+                                                                const uint16_t* __restrict__ eperm, int rounds) {
   constexpr int NBG = NN / NSPLIT, Q = 16;
+  __shared__ uint8_t s_res[kOrderThreads][Q][NBG], s_pick[kOrderThreads][Q][NBG], s_cnt[kOrderThreads][NBG][16];
+  __shared__ int s_mx[kOrderThreads][NBG], s_nmx[kOrderThreads][NBG];
+  auto& res = s_res[threadIdx.x];
+  auto& pick = s_pick[threadIdx.x];
+  auto& cnt = s_cnt[threadIdx.x];
+  auto& mx = s_mx[threadIdx.x];
+  auto& nmx = s_nmx[threadIdx.x];
   const int64_t total = nchunks * groups_per_chunk;
   for (int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gid < total;
        gid += (int64_t)gridDim.x * blockDim.x) {
@@ -3775,8 +3788,6 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
     const float inv = 1.0f / (float)na;
     const int nl = min(Q, nitems - p0);
     uint16_t off[Q][NBG];
-    uint8_t res[Q][NBG], pick[Q][NBG];
-    uint8_t cnt[NBG][16];
     int64_t ent[Q];
     int base[Q];
     const uint16_t* rd = eperm ? src : slots;
@@ -3805,7 +3816,6 @@ __global__ void k_order_slots(const int64_t* __restrict__ row_start, const int64
     }
     // step maxima and how many residues reach them: a swap is then priced in O(1) and the two
     // steps are recounted only when it is taken
-    int mx[NBG], nmx[NBG];
     auto recount = [&](int t) {
       int m = 0, n = 0;
       for (int r = 0; r < 16; ++r) {
@@ -4038,7 +4048,7 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
     if (posn)                                                                                                 \
       k_plan_perm<NN_, NS_><<<grid_for(plan->nchunks), 64, 0, s>>>(plan->row_start, A->indptr, adj->ptr,      \
                                                                    adj->idx, plan->nchunks, src, eperm, eadj);   \
-    k_order_slots<NN_, NS_><<<grid_for(total), 256, 0, s>>>(plan->row_start, A->indptr, adj->ptr, plan->nchunks, \
+    k_order_slots<NN_, NS_><<<grid_for(total, kOrderThreads), kOrderThreads, 0, s>>>(plan->row_start, A->indptr, adj->ptr, plan->nchunks, \
                                                             groups, sl, src, eperm, rounds);                   \
   } while (0)
   bool ok = true;

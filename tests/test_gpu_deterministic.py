@@ -161,3 +161,26 @@ def test_config_e_deterministic_full_size(oracle, dev, n):
     marker, _ = fem._combine_bcs(V, bcs)
     rel, nrows = sampled_row_parity(oracle, V, a, A, marker, nsample=1500)
     assert rel <= RTOL, f"sampled-row parity {rel:.2e} over {nrows} rows"
+
+
+@pytest.mark.parametrize("contrast", [1e2, 1e4])
+def test_deterministic_high_contrast_within_documented_bound(oracle, dev, contrast):
+    """A stiffness jump inside the chunks (E = 1 for x < 0.45, `contrast` beyond): the fixed-point scale is
+    per chunk, set by its stiffest cell, so a row of soft cells in a chunk that also holds stiff rows is
+    summed with the stiff cells' resolution. The documented bound (include/femasm.h FA_DETERMINISTIC):
+    per value within ~2^-50 of the chunk's largest contribution bound per summand; per row at most
+    ~contrast x 1e-13 relative to the row (measured 6.8e-12 at a contrast of 100), so the 1e-12 bar holds
+    up to a contrast of ~10 (the BASELINE E table spans 20: 1e-12 is met there, test above). The default
+    (FP64-atomic) gather meets 1e-12 at every contrast."""
+    from femasm import fem
+
+    m, V, a, bcs = _problem(oracle, -4, 2, (12, 11, 10), dev)
+    xc = m.x[m.cells.to(torch.int64)].mean(1)[:, 0]
+    a.E = torch.where(xc < 0.45, torch.ones_like(xc), torch.full_like(xc, contrast)).contiguous()
+    ref = _oracle(oracle, V, a, bcs)
+    A = fem.assemble_matrix(a, bcs=bcs, deterministic=True)
+    B = fem.assemble_matrix(a, bcs=bcs)
+    ip = A.indptr.cpu().numpy()
+    assert_rows_close(B.data.cpu().numpy(), ref, ip, RTOL)  # the default gather
+    tol = max(RTOL, contrast * 1e-13)
+    assert_rows_close(A.data.cpu().numpy(), ref, ip, tol)

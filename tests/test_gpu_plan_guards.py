@@ -75,3 +75,21 @@ def test_lin_gather_equals_generic_gather(oracle, dev, ct, p, n):
         assert_rows_close(A.data.cpu().numpy(), ref, A.indptr.cpu().numpy(), RTOL)
         out.append(A.data.cpu().numpy())
     assert_rows_close(out[0], out[1], A.indptr.cpu().numpy(), RTOL)
+
+
+@pytest.mark.parametrize("ct,p,n", [(-4, 2, (7, 6, 5)), (-4, 1, (12, 11, 10)), (3, 2, (30, 27))])
+def test_plan_search_equals_oracle(oracle, dev, ct, p, n):
+    """The opt-in alternating-path order search (FA_PLAN_ORDER_SEARCH) only permutes the LDS order of
+    the adds: the matrix equals the oracle's at the per-row bar, like the default plan's."""
+    from femasm import fem, mesh
+
+    m = mesh.create_unit_square(*n, cell_type=ct, device=dev) if len(n) == 2 else \
+        mesh.create_unit_cube(*n, cell_type=ct, device=dev)
+    V = fem.functionspace(m, ("Lagrange", p, (m.gdim,)))
+    E = torch.tensor(oracle.e_range()[np.arange(m.num_cells) % 200], device=dev)
+    a = fem.LinearElasticity(V, E=E, nu=0.3)
+    left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
+    bcs = [fem.dirichletbc(0.0, left, V)]
+    A = fem.assemble_matrix(a, bcs=bcs, plan=dict(owner=False, search=True))
+    marker, _ = fem._combine_bcs(V, bcs)
+    assert_rows_close(A.data.cpu().numpy(), _oracle_vals(oracle, V, a, marker), A.indptr.cpu().numpy(), RTOL)
