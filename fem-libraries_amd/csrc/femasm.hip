@@ -3919,7 +3919,10 @@ __global__ __launch_bounds__(kOrderThreads) void k_order_slots(const int64_t* __
         const int k = pick[q][t];
         v[t] = (uint16_t)(((part * NBG + k) << 10) | (base[q] + off[q][k]));
       }
-      for (int t = 0; t < NBG; ++t) slots[ent[q] + t] = v[t];
+      // one 2-B store each (volatile: not merged into 12- / 16-B stores, whose data registers the
+      // compiler reuses within the gfx950 store-data hazard window; tests/test_store_hazard.py)
+      volatile uint16_t* so = slots + ent[q];
+      for (int t = 0; t < NBG; ++t) so[t] = v[t];
     }
   }
 }

@@ -103,6 +103,10 @@ V = {
     "neo_nostore2": [(
         "    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v[u]), rv, NT * u < lim ? base : OOB, 16 * NT * u, NTS);\n  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, hv), rv, (tid == 0 && h) ? 0 : OOB, 0, NTS);\n  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rv, (tid == 1 && tail) ? 8 * (nv - 1) : OOB, 0, NTS);\n}",
         "    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v[u]), rv, OOB + 0 * lim, 16 * NT * u, NTS);\n  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, hv), rv, OOB, 0, NTS);\n  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rv, OOB + 0 * tail, 0, NTS);\n}")],
+    # (round 5) a 38 KB accumulator for every gather (timing of k_gather_lin on E: larger chunks,
+    # ~120 instead of ~96 entries of the 128 a workgroup's lanes hold)
+    "lin38k": [("constexpr int FA_GATHER_LDS = 32768;", "constexpr int FA_GATHER_LDS = 38912;")],
+    "lin36k": [("constexpr int FA_GATHER_LDS = 32768;", "constexpr int FA_GATHER_LDS = 36864;")],
 }
 
 
