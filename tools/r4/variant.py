@@ -107,6 +107,10 @@ V = {
     # ~120 instead of ~96 entries of the 128 a workgroup's lanes hold)
     "lin38k": [("constexpr int FA_GATHER_LDS = 32768;", "constexpr int FA_GATHER_LDS = 38912;")],
     "lin36k": [("constexpr int FA_GATHER_LDS = 32768;", "constexpr int FA_GATHER_LDS = 36864;")],
+    # the plan's alternating-path search: fewer rounds / shorter chains (round 5)
+    "kr1": [("constexpr int kKempeRounds = 4;", "constexpr int kKempeRounds = 1;")],
+    "kr2": [("constexpr int kKempeRounds = 4;", "constexpr int kKempeRounds = 2;")],
+    "kl3": [("constexpr int kKempeLen = 6;", "constexpr int kKempeLen = 3;")],
 }
 
 

@@ -12,7 +12,7 @@ fi
 for cfg in ${CFGS:-E Eneo C}; do
   for lib in new $B new $B; do
     if [ $lib = new ]; then unset FEMASM_LIB; else export FEMASM_LIB=$PWD/abl/libfemasm_$lib.so; fi
-    timeout -k 10 240 python bench.py --config $cfg --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-hbm-probe --no-eneo \
+    timeout -k 10 240 python bench.py --config $cfg --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-hbm-probe --no-eneo ${EXTRA:-} \
       > gpurun_out/ab_${cfg}_${lib}.json 2> gpurun_out/ab_${cfg}_${lib}.err || { tail -5 gpurun_out/ab_${cfg}_${lib}.err; exit 1; }
     python -c "import json;d=json.load(open('gpurun_out/ab_${cfg}_${lib}.json'));print('$cfg $lib', d['ms_per_step'], d['roofline']['launch_ms'], d['setup']['plan_s'])"
   done
