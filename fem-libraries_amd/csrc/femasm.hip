@@ -79,6 +79,11 @@ struct DevTables {
   const double* ahat;  // simplex only: [nn][nn][td][td] = sum_q w_q dphi_a(q) dphi_b(q)^T
   const double* t1d;   // tensor cells: 1-D matrices S, M, C [3][p+1][p+1] (tensor_1d_mats)
   const double* lat;   // tensor cells: node lattice code a0 + 8 a1 + 64 a2 per node (as doubles)
+  // tensor cells: the 1-D factors of the tabulation (tabulate() in elements.h): Gauss points x[n1],
+  // then the lattice-order 1-D Lagrange values v[n1][p+1] and derivatives dv[n1][p+1] at them;
+  // dphi[q][a][0] = dv[qx][ax] v[qy][ay] v[qz][az] (q = (qx n1 + qy) n1 + qz), bit for bit
+  const double* g1d;
+  int n1q;
   int ndoubles;
   double amax;         // simplex: max |ahat| entry (bounds the blocks of the fixed-point gather)
   // simplex: ahat = N / D with small integers N (exact rational integrals), each block's GD x GD
@@ -179,7 +184,8 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
     }
   }
   // tensor cells: 1-D matrices of the affine fast path and the node lattice codes
-  size_t off_t1d = 0, off_lat = 0;
+  size_t off_t1d = 0, off_lat = 0, off_g1d = 0;
+  int n1q = 0;
   if (!is_simplex(ct)) {
     std::vector<double> t1;
     tensor_1d_mats(p, qd, t1);
@@ -188,6 +194,17 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
     off_lat = h.size();
     std::vector<int> L = tensor_node_lattice(ct, p);
     for (int a = 0; a < T.nn; ++a) h.push_back((double)(L[3 * a] + 8 * L[3 * a + 1] + 64 * L[3 * a + 2]));
+    std::vector<double> gx, gw;
+    gauss_legendre_01((std::max(qd, 1) + 2) / 2, gx, gw);
+    const std::vector<double> r = line_points(p);
+    n1q = (int)gx.size();
+    off_g1d = h.size();
+    h.insert(h.end(), gx.begin(), gx.end());
+    std::vector<double> v1((size_t)n1q * (p + 1)), d1((size_t)n1q * (p + 1));
+    for (int q = 0; q < n1q; ++q)
+      for (int i = 0; i <= p; ++i) lagrange_1d(r, i, gx[q], v1[(size_t)q * (p + 1) + i], d1[(size_t)q * (p + 1) + i]);
+    h.insert(h.end(), v1.begin(), v1.end());
+    h.insert(h.end(), d1.begin(), d1.end());
   }
   double* d = nullptr;
   HIP_TRY(hipMalloc(&d, h.size() * sizeof(double)));
@@ -202,6 +219,8 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
   D.ahat = is_simplex(ct) ? d + off_ahat : nullptr;
   D.t1d = is_simplex(ct) ? nullptr : d + off_t1d;
   D.lat = is_simplex(ct) ? nullptr : d + off_lat;
+  D.g1d = is_simplex(ct) ? nullptr : d + off_g1d;
+  D.n1q = n1q;
   D.ndoubles = (int)h.size();
   D.amax = amax;
   D.pk = off_pk ? reinterpret_cast<const uint64_t*>(d + off_pk) : nullptr;
@@ -295,6 +314,26 @@ struct BsrView {
   int64_t row_end;
 };
 
+// cell_lame in two steps (a load issued early, the arithmetic later): same values bit for bit
+__device__ __forceinline__ void cell_lame_load(const FormView& F, int64_t c, double& a, double& b) {
+  if (F.E) {
+    a = F.E[c];
+    b = 0.0;
+  } else {
+    a = F.lam[c];
+    b = F.mu[c];
+  }
+}
+__device__ __forceinline__ void cell_lame_from(const FormView& F, double a, double b, double& lam, double& mu) {
+  if (F.E) {
+    const double E = a, nu = F.nu;
+    mu = E / (2.0 * (1.0 + nu));
+    lam = E * nu / ((1.0 + nu) * (1.0 - 2.0 * nu));
+  } else {
+    lam = a;
+    mu = b;
+  }
+}
 __device__ __forceinline__ void cell_lame(const FormView& F, int64_t c, double& lam, double& mu) {
   if (F.E) {
     double E = F.E[c], nu = F.nu;
@@ -962,46 +1001,107 @@ __global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
   };
   constexpr int NNP = NT * 16 + 16;   // row stride: +16 doubles puts q and q+1 on opposite bank halves
   constexpr int QMAX = (NQ + 3) & ~3;
+  constexpr int P1 = NN == 8 ? 2 : NN == 27 ? 3 : 4;  // nodes and Gauss points per direction
+  constexpr int G1 = NQ == 8 ? 2 : NQ == 27 ? 3 : 4;
+  static_assert(P1 * P1 * P1 == NN && G1 * G1 * G1 == NQ, "tensor element with a tensor Gauss rule");
   __shared__ double phi[3][QMAX][NNP];
   __shared__ double sJ[QMAX][10];  // Ji (9) + sqrt(w |J|)
-  __shared__ uint8_t s_bcn[NN];    // MODE 2: constrained-dof bits of the cell's nodes
+  __shared__ uint32_t s_bcn[2][NN]; // MODE 2: byte i = dof i of the node constrained (two cells)
+  // round 5: the tables of the per-cell phase (Gauss points, 1-D factors of the basis gradients,
+  // weights, node lattice codes) and the cell's vertices sit in LDS, so the phase before the MFMA
+  // loop issues no global load: a load there waited (vmcnt) for the previous cell's 295 KB of block
+  // stores, which serialised the stores with the next cell (Dmfma: stores ~ MFMA ~ 15 us per cell)
+  __shared__ double s_gx[G1], s_v1[G1][P1], s_d1[G1][P1], s_wq[NQ];
+  __shared__ int s_lat[NN];
+  __shared__ double s_xv[24];      // vertex v, coordinate i at 3 v + i
   static_assert(MODE != 2 || 3 * QMAX * NNP >= NWAVE * 64 * 9, "block staging fits the phi image");
   static_assert(NTL % TPW == 0, "whole waves of tiles");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nq = NQ, nqp = QMAX;
-  for (int64_t ci = blockIdx.x; ci < ncells; ci += gridDim.x) {
+  for (int t = tid; t < NQ; t += NTHR) s_wq[t] = T.wq[t];
+  for (int t = tid; t < NN; t += NTHR) s_lat[t] = (int)T.lat[t];
+  for (int t = tid; t < G1; t += NTHR) s_gx[t] = T.g1d[t];
+  for (int t = tid; t < G1 * P1; t += NTHR) {
+    s_v1[t / P1][t % P1] = T.g1d[G1 + t];
+    s_d1[t / P1][t % P1] = T.g1d[G1 + G1 * P1 + t];
+  }
+  // The next cell's inputs are loaded one cell ahead, their indices two cells ahead: lane tid < 24
+  // holds vertex tid / 3's coordinate tid % 3, lane tid < 3 NN the bc byte of dof tid % 3 of node
+  // tid / 3 (MODE 2; one byte per lane: adjacent byte loads are merged and split at once, which
+  // waits), every lane the cell's material values. Issued after the pre-MFMA phase, consumed after
+  // the MFMA loop.
+  const bool bcb = MODE == 2 && bc != nullptr;
+  auto load_ids = [&](int64_t cc, int32_t& gv, int32_t& nv) {
+    if (cc < ncells) {
+      if (tid < 24) gv = M.geom[(c0 + cc) * 8 + tid / 3];
+      if (bcb && tid < 3 * NN) nv = M.cells[(c0 + cc) * NN + tid / 3];
+    }
+  };
+  auto load_data = [&](int64_t cc, int32_t gv, int32_t nv, double& xval, int& bb, double& la, double& lb) {
+    if (cc < ncells) {
+      if (tid < 24) xval = M.x[(int64_t)gv * 3 + tid % 3];
+      if (bcb && tid < 3 * NN) bb = bc[(int64_t)nv * 3 + tid % 3];
+      cell_lame_load(F, c0 + cc, la, lb);
+    }
+  };
+  uint8_t* const s_bcb = reinterpret_cast<uint8_t*>(&s_bcn[0][0]);
+  auto put_bc = [&](int p, int bb) {
+    if (MODE == 2 && tid < 3 * NN) s_bcb[(p * NN + tid / 3) * 4 + tid % 3] = bb ? 1 : 0;
+  };
+  const int64_t G = gridDim.x;
+  int32_t gv0 = 0, nv0 = 0, gv1 = 0, nv1 = 0;
+  double xval = 0.0, la = 0.0, lb = 0.0;
+  int bits = 0;
+  load_ids(blockIdx.x, gv0, nv0);
+  load_ids(blockIdx.x + G, gv1, nv1);
+  load_data(blockIdx.x, gv0, nv0, xval, bits, la, lb);
+  if (tid < 24) s_xv[tid] = xval;
+  if (MODE == 2) for (int t = tid; t < NN; t += NTHR) s_bcn[0][t] = 0u;
+  if (MODE == 2) for (int t = tid; t < NN; t += NTHR) s_bcn[1][t] = 0u;
+  __syncthreads();
+  put_bc(0, bits);
+  double lam, mu;
+  cell_lame_from(F, la, lb, lam, mu);
+  int par = 0;
+  for (int64_t ci = blockIdx.x; ci < ncells; ci += G, par ^= 1) {
     const int64_t c = c0 + ci;
-    __syncthreads();
-    if (tid < nq) {  // geometry at quadrature point q = tid
-      double xv[8][3];
-      const int32_t* gv = M.geom + c * 8;
+    __syncthreads();  // the previous cell's staging is read; this cell's vertices / bc bits are in LDS
+    if (tid < nq) {   // geometry at quadrature point q = tid (Q1 gradients from the 1-D points)
+      const int qx = tid / (G1 * G1), qy = (tid / G1) % G1, qz = tid % G1;
+      const double xi[3] = {s_gx[qx], s_gx[qy], s_gx[qz]};
+      double xv[8][3], gd[8 * 3];
 #pragma unroll
-      for (int v = 0; v < 8; ++v)
+      for (int v = 0; v < 8; ++v) {
+        double f[3], df[3];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) xv[v][i] = M.x[(int64_t)gv[v] * 3 + i];
+        for (int d = 0; d < 3; ++d) {
+          const bool hi = (v >> d) & 1;
+          f[d] = hi ? xi[d] : 1.0 - xi[d];
+          df[d] = hi ? 1.0 : -1.0;
+        }
+        gd[v * 3 + 0] = df[0] * f[1] * f[2];
+        gd[v * 3 + 1] = f[0] * df[1] * f[2];
+        gd[v * 3 + 2] = f[0] * f[1] * df[2];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) xv[v][i] = s_xv[v * 3 + i];
+      }
       double Ji[3][3];
-      const double det = tensor_geometry<3, 8>(xv, T.gdphi + tid * 24, Ji);
+      const double det = tensor_geometry<3, 8>(xv, gd, Ji);
 #pragma unroll
       for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int k = 0; k < 3; ++k) sJ[tid][i * 3 + k] = Ji[i][k];
-      sJ[tid][9] = sqrt(T.wq[tid] * fabs(det));
-    }
-    if (MODE == 2 && tid < NN) {
-      uint32_t bits = 0u;
-      if (bc) {
-        const int64_t n = M.cells[c * NN + tid];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) bits |= (bc[n * 3 + i] ? 1u : 0u) << i;
-      }
-      s_bcn[tid] = (uint8_t)bits;
+      sJ[tid][9] = sqrt(s_wq[tid] * fabs(det));
     }
     __syncthreads();
-    for (int idx = tid; idx < nqp * NNP; idx += NTHR) {
-      const int q = idx / NNP, a = idx % NNP;
+    for (int idx = tid; idx < nqp * NT * 16; idx += NTHR) {
+      const int q = idx / (NT * 16), a = idx % (NT * 16);
       double g[3] = {0.0, 0.0, 0.0};
       if (q < nq && a < NN) {
-        const double* dp = T.dphi + ((size_t)q * NN + a) * 3;
+        const int qx = q / (G1 * G1), qy = (q / G1) % G1, qz = q % G1;
+        const int lt = s_lat[a], ax = lt & 7, ay = (lt >> 3) & 7, az = lt >> 6;
+        const double vx = s_v1[qx][ax], vy = s_v1[qy][ay], vz = s_v1[qz][az];
+        const double dp[3] = {s_d1[qx][ax] * vy * vz, vx * s_d1[qy][ay] * vz, vx * vy * s_d1[qz][az]};
         const double sc = sJ[q][9];
 #pragma unroll
         for (int d = 0; d < 3; ++d) g[d] = sc * (dp[0] * sJ[q][d] + dp[1] * sJ[q][3 + d] + dp[2] * sJ[q][6 + d]);
@@ -1009,9 +1109,11 @@ __global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
 #pragma unroll
       for (int i = 0; i < 3; ++i) phi[i][q][a] = g[i];
     }
+    // the next cell's inputs (its indices were loaded one cell earlier), the one after's indices
+    int32_t gv2 = 0, nv2 = 0;
+    load_data(ci + G, gv1, nv1, xval, bits, la, lb);
+    load_ids(ci + 2 * G, gv2, nv2);
     __syncthreads();
-    double lam, mu;
-    cell_lame(F, c, lam, mu);
     const int32_t* cn = M.cells + c * NN;
     fa_d4 accs[TPW][9];
 #pragma unroll
@@ -1020,6 +1122,7 @@ __global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
       for (int m = 0; m < 9; ++m) accs[j][m] = fa_d4{0.0, 0.0, 0.0, 0.0};
     {
       const int kq = lane >> 4;
+#pragma unroll 2
       for (int q0 = 0; q0 < nqp; q0 += 4) {
 #pragma unroll
         for (int j = 0; j < TPW; ++j) {
@@ -1041,6 +1144,18 @@ __global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
       }
     }
     if constexpr (MODE == 2) __syncthreads();  // every wave is past its MFMA loop: phi is free
+    // Every load of this iteration is consumed here, before this cell's stores (a value still in
+    // flight when they issue would be waited for behind them): the next cell's vertices and bc bits
+    // go to LDS, its material values and the indices of the cell after it into registers
+    if (ci + G < ncells) {
+      if (tid < 24) s_xv[tid] = xval;
+      put_bc(par ^ 1, bits);
+    }
+    double lam_n, mu_n;
+    cell_lame_from(F, la, lb, lam_n, mu_n);
+    asm volatile("" ::"v"(gv2), "v"(nv2), "v"(lam_n), "v"(mu_n));
+    gv1 = gv2;
+    nv1 = nv2;
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
       int ta, tb;
@@ -1059,7 +1174,9 @@ __global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
           const int a = ta * 16 + (lane >> 4) + 4 * r, b = tb * 16 + (lane & 15);
           if (a < NN && b < NN) {
             const double tr = acc[0][r] + acc[4][r] + acc[8][r];
-            const uint32_t rm = s_bcn[a], cm = s_bcn[b];
+            const uint32_t ra = s_bcn[par][a], rb = s_bcn[par][b];
+            const uint32_t rm = (ra & 1u) | ((ra >> 7) & 2u) | ((ra >> 14) & 4u);
+            const uint32_t cm = (rb & 1u) | ((rb >> 7) & 2u) | ((rb >> 14) & 4u);
 #pragma unroll
             for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -1131,6 +1248,8 @@ __global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
         }
       }
     }
+    lam = lam_n;
+    mu = mu_n;
   }
 }
 
@@ -1196,8 +1315,13 @@ static constexpr int kGatherLdsValues = FA_GATHER_LDS;  // accumulator bytes per
 constexpr int FA_GATHER_LDS_NEO = 46080;
 static constexpr int kGatherLdsNeo = FA_GATHER_LDS_NEO;
 constexpr int FA_NEO_NSPLIT = 2;  // neo-Hookean column items of 5 columns (E-neo at 2 waves / SIMD, round 2: NSPLIT 2
-                                  // 342 ms, 5 at 3 waves 349, 10 at 4 waves 461)
-static constexpr int kGatherNeoEntries = 256 / FA_NEO_NSPLIT;
+                                  // 342 ms, 5 at 3 waves 349, 10 at 4 waves 461; round 5: whole entries, 256
+                                  // per chunk in a 72 KB accumulator, 64.1 vs 64.2 ms, plan 2.5 vs 1.5 s)
+// the neo-Hookean gather's item split per element (launch_gather's instantiations; its plans are
+// ordered for it and capped at 256 / split entries per chunk)
+static int neo_nsplit(int ct, int p) {
+  return ct == FA_TETRAHEDRON && p == 2 ? FA_NEO_NSPLIT : (ct == FA_TRIANGLE && p == 2 ? 2 : 1);
+}
 constexpr int FA_GATHER_ENTRY_CAP = 512;  // adjacency entries per chunk of the default plan (512 = the LDS arrays' cap)
 // blocks of the accumulator of a gather kernel (the plan's chunks must fit it)
 __host__ __device__ constexpr int gather_maxb(bool neo, int bs2) {
@@ -4024,7 +4148,9 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   plan->eadj = nullptr;
   DevTables T;
   if ((rc = get_tables(mesh->cell_type, mesh->degree, -1, &T))) return rc;
-  const int ns = lin_simplex_nsplit(mesh->cell_type, mesh->degree, T.nq, (plan->cell_flags & FA_PLAN_AFFINE) != 0);
+  const int ns = (plan->cell_flags & FA_PLAN_NEO) && is_simplex(mesh->cell_type)
+                     ? neo_nsplit(mesh->cell_type, mesh->degree)
+                     : lin_simplex_nsplit(mesh->cell_type, mesh->degree, T.nq, (plan->cell_flags & FA_PLAN_AFFINE) != 0);
   if (ns == 0 || plan->nchunks <= 0) return FA_OK;  // no kernel reads an ordered map: keep plain slots
   // ordered entries pack (b << 10) | chunk-relative position (k_order_slots): keep the plain map
   // for a plan whose chunks could hold 1024 blocks or more
@@ -4198,8 +4324,10 @@ extern "C" int fa_plan_gather_form(const fa_mesh* mesh, int32_t kind, const fa_a
                                    int64_t* row_start, fa_plan* plan, void* stream) {
   if (!mesh) return fail(FA_E_ARG, "null mesh");
   if (kind != FA_NEO_HOOKEAN) return fa_plan_gather(mesh, adj, A, row_start, plan, stream);
-  return plan_gather(mesh, adj, A, row_start, plan, stream, gather_maxb(true, mesh->gdim * mesh->gdim),
-                     kGatherNeoEntries);
+  const int rc = plan_gather(mesh, adj, A, row_start, plan, stream, gather_maxb(true, mesh->gdim * mesh->gdim),
+                             256 / neo_nsplit(mesh->cell_type, mesh->degree));
+  if (rc == FA_OK) plan->cell_flags |= FA_PLAN_NEO;
+  return rc;
 }
 
 // ------------------------------------------------------------------------------- contribution plan

@@ -17,7 +17,7 @@ FA_OK = 0
 FA_TRIANGLE, FA_QUADRILATERAL, FA_TETRAHEDRON, FA_HEXAHEDRON = 3, 4, -4, 8
 FA_LINEAR_ELASTICITY, FA_ASYM_DAMAGE, FA_NEO_HOOKEAN, FA_ASYM_DAMAGE_AD = 0, 1, 2, 3
 FA_GATHER, FA_SCATTER, FA_ZERO_FIRST, FA_DETERMINISTIC, FA_CHECK_ERRORS = 0x0, 0x1, 0x2, 0x4, 0x8
-FA_PLAN_AFFINE, FA_PLAN_DETERMINISTIC, FA_PLAN_ORDER_SEARCH = 0x1, 0x2, 0x4
+FA_PLAN_AFFINE, FA_PLAN_DETERMINISTIC, FA_PLAN_ORDER_SEARCH, FA_PLAN_NEO = 0x1, 0x2, 0x4, 0x8
 
 
 class FemasmError(RuntimeError):

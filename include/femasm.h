@@ -133,7 +133,9 @@ typedef struct {
                                      fa_gather_rows) are deterministic, as with FA_DETERMINISTIC */
 #define FA_PLAN_ORDER_SEARCH 0x4  /* set by the caller before fa_plan_order: also run the alternating-path
                                      moves of the bank-order search (fewer LDS bank conflicts, config E
-                                     ~0.5 % faster per assembly, plan ~10x slower: 1.7 -> 20 s) */
+                                     ~0.7 % faster per assembly, plan ~8x slower: 1.5 -> 12 s) */
+#define FA_PLAN_NEO 0x8           /* set by fa_plan_gather_form for FA_NEO_HOOKEAN: fa_plan_order orders
+                                     the slots for the neo-Hookean kernel's item split */
 
 /* Row-chunk plan for the gather kernel (host-computed once per pattern). */
 typedef struct {

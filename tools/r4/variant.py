@@ -111,12 +111,30 @@ V = {
     "kr1": [("constexpr int kKempeRounds = 4;", "constexpr int kKempeRounds = 1;")],
     "kr2": [("constexpr int kKempeRounds = 4;", "constexpr int kKempeRounds = 2;")],
     "kl3": [("constexpr int kKempeLen = 6;", "constexpr int kKempeLen = 3;")],
+    # neo_timing with the next chunk's record loads counted in "items" (applied after neo_timing)
+    "neo_tload": [("    FN_T(0);\n    // chunk k+1's records / slots / masks: the item registers are dead here, and these loads are\n",
+                   "    // chunk k+1's records / slots / masks: the item registers are dead here, and these loads are\n"),
+                  ("    load_item(d1, pf1, cur);\n    __syncthreads();  // B1: the chunk is accumulated\n    FN_T(1);",
+                   "    load_item(d1, pf1, cur);\n    FN_T(0);\n    __syncthreads();  // B1: the chunk is accumulated\n    FN_T(1);")],
+    # positional plans without the bank-balancing entry placement: position = adjacency order
+    # (entries of a row, and of neighbouring rows, share cells: lanes of a quarter read nearby records)
+    "perm_id": [("      const int j = gather_perm(jj, na, st, inv);\n      const int64_t e = a0 + j;\n      int64_t lo = r0, hi = r1 - 1;\n      while (lo < hi) {\n        const int64_t mid = (lo + hi + 1) >> 1;\n        if (adj_ptr[mid] <= e) lo = mid; else hi = mid - 1;\n      }\n      const int rowlo = (int)(indptr[lo] - b0);\n      uint8_t res[NN];",
+                 "      const int j = jj;\n      const int64_t e = a0 + j;\n      int64_t lo = r0, hi = r1 - 1;\n      while (lo < hi) {\n        const int64_t mid = (lo + hi + 1) >> 1;\n        if (adj_ptr[mid] <= e) lo = mid; else hi = mid - 1;\n      }\n      const int rowlo = (int)(indptr[lo] - b0);\n      uint8_t res[NN];"),
+                ("      const int pos = best * EQ + fill[best];", "      const int pos = jj;")],
+    # the neo-Hookean gather with items of whole entries (10 columns, 256 per chunk) instead of 5 columns
+    "neo1": [("constexpr int FA_GATHER_LDS_NEO = 46080;", "constexpr int FA_GATHER_LDS_NEO = 1022 * 72;"),
+             ("constexpr int FA_NEO_NSPLIT = 2;", "constexpr int FA_NEO_NSPLIT = 1;")],
 }
+
+
+def subs(name):
+    """a variant name, or several joined by '+' (applied in order)"""
+    return [x for n in name.split("+") for x in V[n]]
 
 
 def build(name):
     src = open(SRC).read()
-    for old, new in V[name]:
+    for old, new in subs(name):
         if old not in src:
             raise SystemExit(f"variant {name}: pattern not found:\n{old}")
         src = src.replace(old, new)
@@ -131,11 +149,12 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["--list"]:
         print("\n".join(V))
         raise SystemExit(0)
-    src = open(SRC).read()
-    for n in sys.argv[1:]:  # every pattern checked before any build starts
-        for old, _ in V[n]:
+    for n in sys.argv[1:]:  # every pattern checked (in order) before any build starts
+        src = open(SRC).read()
+        for old, new in subs(n):
             if old not in src:
                 raise SystemExit(f"variant {n}: pattern not found:\n{old}")
+            src = src.replace(old, new)
     procs = [build(n) for n in sys.argv[1:]]
     rc = 0
     for p, path in procs:
