@@ -999,7 +999,9 @@ __global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
     ta = t / NT;
     tb = t % NT;
   };
-  constexpr int NNP = NT * 16 + 16;   // row stride: +16 doubles puts q and q+1 on opposite bank halves
+  // row stride: +8 doubles puts the 4 rows q0..q0+3 a ds_read_b64 of the MFMA loop reads on 2 banks
+  // each (2 passes, the minimum for 512 B); round 2's +16 left no room for the staging below
+  constexpr int NNP = NT * 16 + 8;
   constexpr int QMAX = (NQ + 3) & ~3;
   constexpr int P1 = NN == 8 ? 2 : NN == 27 ? 3 : 4;  // nodes and Gauss points per direction
   constexpr int G1 = NQ == 8 ? 2 : NQ == 27 ? 3 : 4;
@@ -1014,9 +1016,9 @@ __global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
   __shared__ double s_gx[G1], s_v1[G1][P1], s_d1[G1][P1], s_wq[NQ];
   __shared__ int s_lat[NN];
   __shared__ double s_xv[24];      // vertex v, coordinate i at 3 v + i
-  static_assert(MODE != 2 || 3 * QMAX * NNP >= NWAVE * 64 * 9, "block staging fits the phi image");
+  __shared__ double s_st[MODE == 2 ? NWAVE : 1][64 * 9];  // MODE 2: each wave's block staging
   static_assert(NTL % TPW == 0, "whole waves of tiles");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nq = NQ, nqp = QMAX;
   for (int t = tid; t < NQ; t += NTHR) s_wq[t] = T.wq[t];
   for (int t = tid; t < NN; t += NTHR) s_lat[t] = (int)T.lat[t];
@@ -1115,20 +1117,22 @@ __global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
     load_ids(ci + 2 * G, gv2, nv2);
     __syncthreads();
     const int32_t* cn = M.cells + c * NN;
-    fa_d4 accs[TPW][9];
+    double lam_n = 0.0, mu_n = 0.0;
+    // The wave's tiles one after the other (round 5): tile j's stores drain while tile j + 1's MFMA
+    // loop runs (both tiles' accumulators at once kept the stores after every MFMA of the cell), and
+    // 9 accumulators instead of 18 leave registers free
 #pragma unroll
-    for (int j = 0; j < TPW; ++j)
+    for (int j = 0; j < TPW; ++j) {
+      int ta, tb;
+      tile_of(wave + j * NWAVE, ta, tb);
+      fa_d4 acc[9];
 #pragma unroll
-      for (int m = 0; m < 9; ++m) accs[j][m] = fa_d4{0.0, 0.0, 0.0, 0.0};
-    {
-      const int kq = lane >> 4;
+      for (int m = 0; m < 9; ++m) acc[m] = fa_d4{0.0, 0.0, 0.0, 0.0};
+      {
+        const int kq = lane >> 4;
+        const int ra = ta * 16 + (lane & 15), rb = tb * 16 + (lane & 15);
 #pragma unroll 2
-      for (int q0 = 0; q0 < nqp; q0 += 4) {
-#pragma unroll
-        for (int j = 0; j < TPW; ++j) {
-          int ta, tb;
-          tile_of(wave + j * NWAVE, ta, tb);
-          const int ra = ta * 16 + (lane & 15), rb = tb * 16 + (lane & 15);
+        for (int q0 = 0; q0 < nqp; q0 += 4) {
           double av[3], bv[3];
 #pragma unroll
           for (int i = 0; i < 3; ++i) {
@@ -1139,35 +1143,28 @@ __global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
           for (int i = 0; i < 3; ++i)
 #pragma unroll
             for (int k = 0; k < 3; ++k)
-              accs[j][i * 3 + k] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[k], accs[j][i * 3 + k], 0, 0, 0);
+              acc[i * 3 + k] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[k], acc[i * 3 + k], 0, 0, 0);
         }
       }
-    }
-    if constexpr (MODE == 2) __syncthreads();  // every wave is past its MFMA loop: phi is free
-    // Every load of this iteration is consumed here, before this cell's stores (a value still in
-    // flight when they issue would be waited for behind them): the next cell's vertices and bc bits
-    // go to LDS, its material values and the indices of the cell after it into registers
-    if (ci + G < ncells) {
-      if (tid < 24) s_xv[tid] = xval;
-      put_bc(par ^ 1, bits);
-    }
-    double lam_n, mu_n;
-    cell_lame_from(F, la, lb, lam_n, mu_n);
-    asm volatile("" ::"v"(gv2), "v"(nv2), "v"(lam_n), "v"(mu_n));
-    gv1 = gv2;
-    nv1 = nv2;
-#pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-      int ta, tb;
-      tile_of(wave + j * NWAVE, ta, tb);
-      const fa_d4 (&acc)[9] = accs[j];
+      if (j == 0) {
+        // Every load of this iteration is consumed here, before this cell's stores (a value still
+        // in flight when they issue would be waited for behind them): the next cell's vertices and
+        // bc bits go to LDS, its material values and the indices of the cell after it into registers
+        if (ci + G < ncells) {
+          if (tid < 24) s_xv[tid] = xval;
+          put_bc(par ^ 1, bits);
+        }
+        cell_lame_from(F, la, lb, lam_n, mu_n);
+        asm volatile("" ::"v"(gv2), "v"(nv2), "v"(lam_n), "v"(mu_n));
+        gv1 = gv2;
+        nv1 = nv2;
+      }
       // D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * r
       if constexpr (MODE == 2) {
         // block store for the row gather, Eb[c][a][b][3][3] with bc rows / columns zeroed: the
-        // wave's 4 x 16 blocks of each r go through a wave-private slice of the (now unused) phi
-        // image and leave as contiguous 8-B-per-lane stores (512 B per instruction), instead of
-        // nine 72-B-strided stores per lane
-        double* st = &phi[0][0][0] + wave * (64 * 9);
+        // wave's 4 x 16 blocks of each r go through its own LDS staging and leave as contiguous
+        // stores (512 B / 1 KB per instruction), instead of nine 72-B-strided stores per lane
+        double* st = s_st[wave];
         const int nbv = min(16, NN - tb * 16);  // valid column blocks of this tile
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1189,11 +1186,34 @@ __global__ __launch_bounds__(hex_threads_m(NN, MODE)) void k_hex_mfma(
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           // row j of the 4: blocks [tb*16, tb*16 + nbv) of row a_j are contiguous in Eb
-          const int nrow = nbv * 9;
-          for (int t = lane; t < 4 * nrow; t += 64) {
-            const int j = t / nrow, off = t - j * nrow;
-            const int aj = ta * 16 + j + 4 * r;
-            if (aj < NN) Ae[((ci * NN + aj) * NN + tb * 16) * 9 + off] = st[j * 144 + off];
+          if constexpr (NN % 16 == 0) {
+            // whole 16-block rows (Q3): 4 x 72 16-B pairs, lane pair P = lane + 64 u of row P / 72,
+            // stored with buffer stores whose offsets are per-lane constants (round 5: the generic
+            // loop below spent ~60 VALU per 8-B store on its index arithmetic, and its store phase
+            // took ~35 % of the cell's clocks)
+            typedef int v4i __attribute__((ext_vector_type(4)));
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                Ae + ((ci * NN + ta * 16 + 4 * r) * NN + tb * 16) * 9, 0, (3 * NN * 9 + 144) * 8, 0x00020000);
+            const fa_dv2* s2 = reinterpret_cast<const fa_dv2*>(st);
+            fa_dv2 v[5];
+#pragma unroll
+            for (int u = 0; u < 5; ++u) v[u] = s2[u < 4 || lane < 32 ? lane + 64 * u : 0];  // all reads first
+#pragma unroll
+            for (int u = 0; u < 5; ++u) {
+              const int P = lane + 64 * u;
+              if (u < 4 || P < 288) {
+                const int j = P / 72, q = P - 72 * j;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v[u]), rs, (j * NN * 9 + 2 * q) * 8, 0, 0);
+                store_guard1(v[u]);
+              }
+            }
+          } else {
+            const int nrow = nbv * 9;
+            for (int t = lane; t < 4 * nrow; t += 64) {
+              const int j = t / nrow, off = t - j * nrow;
+              const int aj = ta * 16 + j + 4 * r;
+              if (aj < NN) Ae[((ci * NN + aj) * NN + tb * 16) * 9 + off] = st[j * 144 + off];
+            }
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
@@ -5123,6 +5143,8 @@ static int launch_hex_gather(GatherArgs P, const DevTables& T, const int8_t* bc,
   }
   if (nc > 0 && W.mode != GatherStage::ROWS) {
     constexpr int thr = hex_threads_m(NN, 2);
+    // one workgroup per cell (a resident grid looping over the cells with the next cell's inputs
+    // prefetched measured 41.7 vs 41.5 ms on config Dmfma, round 5)
     const int grid = (int)std::min<int64_t>(nc, kMaxBlocks);
     BsrView none{nullptr, nullptr, nullptr, 0, 0};
     k_hex_mfma<NN, NQ, 2><<<grid, thr, 0, s>>>(P.M, P.F, T, 0, nc, eb, none, bc, P.err);

@@ -116,6 +116,17 @@ V = {
                    "    // chunk k+1's records / slots / masks: the item registers are dead here, and these loads are\n"),
                   ("    load_item(d1, pf1, cur);\n    __syncthreads();  // B1: the chunk is accumulated\n    FN_T(1);",
                    "    load_item(d1, pf1, cur);\n    FN_T(0);\n    __syncthreads();  // B1: the chunk is accumulated\n    FN_T(1);")],
+    # per-phase clocks of k_hex_mfma (block 0's waves print their sums at exit): pre-MFMA phase, MFMA
+    # loop, post-MFMA barrier + next-cell consume, block stores
+    "hex_timing": [("  int par = 0;\n", "  int par = 0;\n  unsigned long long h_t[4] = {0, 0, 0, 0}, h_p = __builtin_amdgcn_s_memtime();\n"
+                    "#define FH_T(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); h_t[i] += t_ - h_p; h_p = t_; }\n"),
+                   ("    load_ids(ci + 2 * G, gv2, nv2);\n    __syncthreads();\n", "    load_ids(ci + 2 * G, gv2, nv2);\n    __syncthreads();\n    FH_T(0);\n"),
+                   ("    if constexpr (MODE == 2) __syncthreads();  // every wave is past its MFMA loop: phi is free\n",
+                    "    FH_T(1);\n    if constexpr (MODE == 2) __syncthreads();  // every wave is past its MFMA loop: phi is free\n"),
+                   ("    gv1 = gv2;\n    nv1 = nv2;\n#pragma unroll\n    for (int j = 0; j < TPW; ++j) {\n      int ta, tb;",
+                    "    gv1 = gv2;\n    nv1 = nv2;\n    FH_T(2);\n#pragma unroll\n    for (int j = 0; j < TPW; ++j) {\n      int ta, tb;"),
+                   ("    lam = lam_n;\n    mu = mu_n;\n  }\n}\n",
+                    "    lam = lam_n;\n    mu = mu_n;\n    FH_T(3);\n  }\n  if (blockIdx.x < 2 && lane == 0) printf(\"hex_timing %d %d %llu %llu %llu %llu\\n\", (int)blockIdx.x, wave, h_t[0], h_t[1], h_t[2], h_t[3]);\n}\n")],
     # positional plans without the bank-balancing entry placement: position = adjacency order
     # (entries of a row, and of neighbouring rows, share cells: lanes of a quarter read nearby records)
     "perm_id": [("      const int j = gather_perm(jj, na, st, inv);\n      const int64_t e = a0 + j;\n      int64_t lo = r0, hi = r1 - 1;\n      while (lo < hi) {\n        const int64_t mid = (lo + hi + 1) >> 1;\n        if (adj_ptr[mid] <= e) lo = mid; else hi = mid - 1;\n      }\n      const int rowlo = (int)(indptr[lo] - b0);\n      uint8_t res[NN];",
