@@ -2924,9 +2924,10 @@ __host__ __device__ constexpr int sym_pair(int j, int l) {
 }
 
 // NeoM records, one wave per 64-cell tile (lane = cell), each block of the tile staged in
-// wave-private LDS and stored as one contiguous run (as k_neo_records_tiled)
+// wave-private LDS and stored as one contiguous run (as k_neo_records_tiled). 3 waves / SIMD (168
+// VGPRs, 2 spilled outside the point loop): E-neo 64.3 vs 65.2 ms at 2 (195 VGPRs), 68.4 at 4
 template <int GD, int NN, int NQ>
-__global__ __launch_bounds__(256) void k_neo_records_m(MeshView M, FormView F, const double* __restrict__ tab,
+__global__ __launch_bounds__(256, 3) void k_neo_records_m(MeshView M, FormView F, const double* __restrict__ tab,
                                                        const int8_t* __restrict__ bc, double* __restrict__ rec,
                                                        uint32_t* __restrict__ bcmask) {
   using R = NeoM<GD, NQ>;

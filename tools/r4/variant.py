@@ -127,6 +127,9 @@ V = {
                     "    gv1 = gv2;\n    nv1 = nv2;\n    FH_T(2);\n#pragma unroll\n    for (int j = 0; j < TPW; ++j) {\n      int ta, tb;"),
                    ("    lam = lam_n;\n    mu = mu_n;\n  }\n}\n",
                     "    lam = lam_n;\n    mu = mu_n;\n    FH_T(3);\n  }\n  if (blockIdx.x < 2 && lane == 0) printf(\"hex_timing %d %d %llu %llu %llu %llu\\n\", (int)blockIdx.x, wave, h_t[0], h_t[1], h_t[2], h_t[3]);\n}\n")],
+    # k_neo_records_m occupancy: 2 waves / SIMD (195 VGPRs) or 4 (128)
+    "nr2": [("__global__ __launch_bounds__(256, 3) void k_neo_records_m(", "__global__ __launch_bounds__(256) void k_neo_records_m(")],
+    "nr4": [("__global__ __launch_bounds__(256, 3) void k_neo_records_m(", "__global__ __launch_bounds__(256, 4) void k_neo_records_m(")],
     # positional plans without the bank-balancing entry placement: position = adjacency order
     # (entries of a row, and of neighbouring rows, share cells: lanes of a quarter read nearby records)
     "perm_id": [("      const int j = gather_perm(jj, na, st, inv);\n      const int64_t e = a0 + j;\n      int64_t lo = r0, hi = r1 - 1;\n      while (lo < hi) {\n        const int64_t mid = (lo + hi + 1) >> 1;\n        if (adj_ptr[mid] <= e) lo = mid; else hi = mid - 1;\n      }\n      const int rowlo = (int)(indptr[lo] - b0);\n      uint8_t res[NN];",
