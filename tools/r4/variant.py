@@ -130,6 +130,13 @@ V = {
     # k_neo_records_m occupancy: 2 waves / SIMD (195 VGPRs) or 4 (128)
     "nr2": [("__global__ __launch_bounds__(256, 3) void k_neo_records_m(", "__global__ __launch_bounds__(256) void k_neo_records_m(")],
     "nr4": [("__global__ __launch_bounds__(256, 3) void k_neo_records_m(", "__global__ __launch_bounds__(256, 4) void k_neo_records_m(")],
+    # k_gather_lin's chunk stores: cache policy bits of the buffer stores (2 = nt, the default)
+    "nts0": [("      constexpr int OOB = 0x40000000, NTS = 2;  // nt\n      // one descriptor over the chunk's nv values",
+              "      constexpr int OOB = 0x40000000, NTS = 0;  // nt\n      // one descriptor over the chunk's nv values")],
+    "nts1": [("      constexpr int OOB = 0x40000000, NTS = 2;  // nt\n      // one descriptor over the chunk's nv values",
+              "      constexpr int OOB = 0x40000000, NTS = 1;  // nt\n      // one descriptor over the chunk's nv values")],
+    "nts3": [("      constexpr int OOB = 0x40000000, NTS = 2;  // nt\n      // one descriptor over the chunk's nv values",
+              "      constexpr int OOB = 0x40000000, NTS = 3;  // nt\n      // one descriptor over the chunk's nv values")],
     # positional plans without the bank-balancing entry placement: position = adjacency order
     # (entries of a row, and of neighbouring rows, share cells: lanes of a quarter read nearby records)
     "perm_id": [("      const int j = gather_perm(jj, na, st, inv);\n      const int64_t e = a0 + j;\n      int64_t lo = r0, hi = r1 - 1;\n      while (lo < hi) {\n        const int64_t mid = (lo + hi + 1) >> 1;\n        if (adj_ptr[mid] <= e) lo = mid; else hi = mid - 1;\n      }\n      const int rowlo = (int)(indptr[lo] - b0);\n      uint8_t res[NN];",
