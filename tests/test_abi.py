@@ -78,3 +78,20 @@ def test_library_reads_no_environment():
             txt = open(os.path.join(pkg, f)).read()
             names = set(re.findall(r"FEMASM_[A-Z_]+", txt)) - {"FEMASM_LIB"}
             assert not names and "os.environ" not in txt.replace('os.environ.get("FEMASM_LIB")', ""), f
+
+
+def test_python_constants_match_header():
+    """Every FA_* integer constant the host package defines equals the header's #define (or enum
+    value) of the same name: the ctypes layer passes them to the library as plain integers."""
+    from femasm import _lib
+
+    txt = open(HEADER).read()
+    hdr = {m.group(1): int(m.group(2), 0)
+           for m in re.finditer(r"#define\s+(FA_[A-Z0-9_]+)\s+\(?(-?(?:0x[0-9A-Fa-f]+|\d+))\)?", txt)}
+    hdr.update({m.group(1): int(m.group(2), 0) for m in re.finditer(r"\b(FA_[A-Z0-9_]+)\s*=\s*(-?(?:0x[0-9A-Fa-f]+|\d+))", txt)})
+    py = {k: v for k, v in vars(_lib).items() if k.startswith("FA_") and isinstance(v, int)}
+    assert py, "no FA_ constants in femasm._lib"
+    missing = sorted(k for k in py if k not in hdr)
+    assert not missing, f"not in include/femasm.h: {missing}"
+    for k, v in py.items():
+        assert hdr[k] == v, f"{k}: header {hdr[k]}, femasm._lib {v}"
