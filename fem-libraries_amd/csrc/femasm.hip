@@ -1420,7 +1420,8 @@ struct GatherArgs {
   const double* lat;  // MAT_AFFT: node lattice codes a0 + 8 a1 + 64 a2
   const double* rec;  // [ncells][Rec::SIZE]
   const uint32_t* bcmask;  // [ncells] or NULL
-  const uint8_t* nodemask; // fused P1 records (k_gather_lin FUSE): [nnodes] constrained-dof bits, or NULL
+  const double* xpack;      // fused P1 records (k_gather_lin FUSE): [nnodes][4] = the node's coordinates
+                            // and its constrained-dof bits (as the bits of a double), k_pack_nodes
   int* err;
   // deterministic assembly (FA_DETERMINISTIC): k_gather_lin accumulates 64-bit fixed point (integer
   // LDS atomics, order-independent sums); fixc bounds an item's block entries by fixc * rho^2,
@@ -2490,7 +2491,6 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
   if (tid < 2) s_fx[tid] = 0u;
 
   const int32_t* __restrict__ eadj = P.eadj;
-  const uint32_t mkmul = P.bcmask ? 1u : 0u;  // FUSE: "has bcs" (the node bits are read only then)
   // a chunk: first block and adjacency entry, block and entry counts (< 2^31 each: fa_plan_gather's caps);
   // 6 SGPRs, and up to five in flight
   struct Desc { int64_t b0, a0; int32_t nb, na; };  // b0 relative to the window's first block
@@ -2535,12 +2535,15 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
       uint32_t m = 0u;
 #pragma unroll
       for (int t = 0; t < NV1; ++t) {
-#pragma unroll
-        for (int i = 0; i < GD; ++i) it.x[t][i] = P.M.x[(int64_t)vd.v[t] * GD + i];
-        m |= (uint32_t)P.nodemask[(int64_t)vd.v[t] * mkmul] << (t * GD);  // no bcs: P.nodemask[0] of a zero line
+        const fa_dv2* pn = reinterpret_cast<const fa_dv2*>(P.xpack + 4 * (int64_t)vd.v[t]);
+        const fa_dv2 a = pn[0], b = pn[1];
+        it.x[t][0] = a.x;
+        it.x[t][1] = a.y;
+        if constexpr (GD == 3) it.x[t][GD - 1] = b.x;
+        m |= (uint32_t)__double_as_longlong(GD == 3 ? b.y : b.x) << (t * GD);
       }
       it.E = P.F.E[c];
-      it.mask = m * mkmul;
+      it.mask = m;
     } else {
       const dv2* rp = reinterpret_cast<const dv2*>(P.rec + c * RL);
 #pragma unroll
@@ -4826,14 +4829,26 @@ struct GatherStage {
 };
 static inline int64_t align256(int64_t b) { return (b + 255) & ~int64_t(255); }
 
-// constrained-dof bits of every node (bit j: dof node * GD + j), for the fused P1 records
+// every node's coordinates and constrained-dof bits (bit j: dof node * GD + j), for the fused P1 records
 template <int GD>
-__global__ void k_node_bcmask(const int8_t* __restrict__ bc, int64_t nnodes, uint8_t* __restrict__ out) {
+__global__ void k_pack_nodes(const double* __restrict__ x, const int8_t* __restrict__ bc, int64_t nnodes,
+                             double* __restrict__ out) {
+  // node n -> {x, y, z, bits} (GD = 3) or {x, y, bits, 0} (GD = 2): one vertex in two 16-B loads of
+  // the fused gather (its coordinates were GD 8-B loads and its bc bits a byte load), round 5
   for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < nnodes; n += (int64_t)gridDim.x * blockDim.x) {
     uint32_t m = 0u;
+    if (bc) {
 #pragma unroll
-    for (int j = 0; j < GD; ++j) m |= (bc[n * GD + j] ? 1u : 0u) << j;
-    out[n] = (uint8_t)m;
+      for (int j = 0; j < GD; ++j) m |= (bc[n * GD + j] ? 1u : 0u) << j;
+    }
+    const double mb = __longlong_as_double((long long)m);
+    const fa_dv2 a = fa_dv2{x[n * GD], x[n * GD + 1]};
+    const fa_dv2 b = GD == 3 ? fa_dv2{x[n * GD + GD - 1], mb} : fa_dv2{mb, 0.0};
+    fa_dv2* o = reinterpret_cast<fa_dv2*>(out + 4 * n);
+    o[0] = a;
+    store_guard1(a);
+    o[1] = b;
+    store_guard1(b);
   }
 }
 
@@ -4975,18 +4990,20 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   if constexpr (MAT == MAT_LINU && R::SIMP && NN == GD + 1 && NN % NSPLIT == 0 && FA_LIN_FUSE) {
     // P1 simplices through fa_assemble_matrix: k_gather_lin forms the records itself (FUSE)
     constexpr int LNT = lin_threads(GD, NN);
-    if (W.mode == GatherStage::FULL && P.nchunks > 0 && P.F.E && !P.cw && P.eadj &&
+    // (the fused items read their vertices' bc bits by geometry node: the same numbering as the
+    // dofmap's, which P1 shares -- another dofmap takes the records path below)
+    if (W.mode == GatherStage::FULL && P.nchunks > 0 && P.F.E && !P.cw && P.eadj && P.M.geom == P.M.cells &&
         P.slots && P.slot_order == NSPLIT && !P.corder && P.plan_maxadj * NSPLIT <= LNT && P.plan_maxadj >= 0 &&
         P.plan_maxb <= lin_maxb(GD, NN) && P.nchunks < (1ll << 31)) {
       int rc;
-      uint8_t* nm = nullptr;
-      if (bc) {
-        if ((rc = scratch_alloc((void**)&nm, (size_t)P.M.nnodes, s))) return rc;
-        k_node_bcmask<GD><<<grid_for(P.M.nnodes), 256, 0, s>>>(bc, P.M.nnodes, nm);
+      double* xp = nullptr;
+      if ((rc = scratch_alloc((void**)&xp, sizeof(double) * 4 * (size_t)std::max<int64_t>(P.M.nnodes, 1), s))) return rc;
+      if (P.M.nnodes > 0) {
+        k_pack_nodes<GD><<<grid_for(P.M.nnodes), 256, 0, s>>>(P.M.x, bc, P.M.nnodes, xp);
         LAUNCH_CHECK();
       }
-      P.nodemask = nm;
-      P.bcmask = nm ? reinterpret_cast<const uint32_t*>(nm) : nullptr;  // only "has bcs" is read
+      P.xpack = xp;
+      P.bcmask = bc ? reinterpret_cast<const uint32_t*>(xp) : nullptr;  // only "has bcs" is read
       P.rec = nullptr;
       const double nu = P.F.nu;
       P.rlm = 2.0 * nu / (1.0 - 2.0 * nu);
@@ -4994,7 +5011,6 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       uint32_t* zero32 = nullptr;
       double* dump = nullptr;
       if ((rc = lin_scratch(&zero32, &dump))) return rc;
-      if (!nm) P.nodemask = reinterpret_cast<const uint8_t*>(zero32);  // a valid address (mask scaled by 0)
       P.fixc = lin_fix_bound(GD, NN, P.rlm, P.trc, P.amax);
       int64_t* ldesc = nullptr;
       if ((rc = lin_chunk_desc(P, &ldesc, s, seq))) return rc;
@@ -5010,8 +5026,8 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       if (bc) {
         k_bc_diag<GD><<<grid_for((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
         LAUNCH_CHECK();
-        HIP_TRY(hipFreeAsync(nm, s));
       }
+      HIP_TRY(hipFreeAsync(xp, s));
       return FA_OK;
     }
   }
@@ -5299,7 +5315,7 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;
-    P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr; P.nodemask = nullptr;
+    P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr; P.xpack = nullptr;
     P.affine = (plan->cell_flags & FA_PLAN_AFFINE) != 0;
     P.t1d = T.t1d; P.lat = T.lat;
     P.fix = ((flags & FA_DETERMINISTIC) || (plan->cell_flags & FA_PLAN_DETERMINISTIC)) ? 1 : 0;

@@ -137,6 +137,8 @@ V = {
               "      constexpr int OOB = 0x40000000, NTS = 1;  // nt\n      // one descriptor over the chunk's nv values")],
     "nts3": [("      constexpr int OOB = 0x40000000, NTS = 2;  // nt\n      // one descriptor over the chunk's nv values",
               "      constexpr int OOB = 0x40000000, NTS = 3;  // nt\n      // one descriptor over the chunk's nv values")],
+    # P1 simplices through the records kernel + k_gather_lin (no fused records)
+    "nofuse": [("constexpr int FA_LIN_FUSE = 1;", "constexpr int FA_LIN_FUSE = 0;")],
     # positional plans without the bank-balancing entry placement: position = adjacency order
     # (entries of a row, and of neighbouring rows, share cells: lanes of a quarter read nearby records)
     "perm_id": [("      const int j = gather_perm(jj, na, st, inv);\n      const int64_t e = a0 + j;\n      int64_t lo = r0, hi = r1 - 1;\n      while (lo < hi) {\n        const int64_t mid = (lo + hi + 1) >> 1;\n        if (adj_ptr[mid] <= e) lo = mid; else hi = mid - 1;\n      }\n      const int rowlo = (int)(indptr[lo] - b0);\n      uint8_t res[NN];",
