@@ -4,7 +4,7 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 for c in ${CFGS:-E C}; do
-for d in "" "--deterministic"; do
+for d in ${DETS:-"" "--deterministic"}; do
   FEMASM_LIB=$PWD/abl/libfemasm_lin_timing.so timeout -k 10 300 python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline --no-hbm-probe $d > gpurun_out/t_$c$d.out 2> gpurun_out/t_$c$d.err || { echo "$c $d failed"; tail -5 gpurun_out/t_$c$d.err; exit 1; }
   python - gpurun_out/t_$c$d.out "$c $d" <<'PY'
 import sys, json
