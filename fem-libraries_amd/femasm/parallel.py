@@ -145,6 +145,16 @@ def bc_diagonal_fixups(part: SlabPartition, indptr: torch.Tensor, indices: torch
     return out if out.numel() else None
 
 
+def _host_staged_ready(t: torch.Tensor, group) -> None:
+    """gloo (the CPU rehearsal backend) copies a device tensor to the host on its own thread, without
+    waiting for the work queued on the current stream: the tensor must be complete before the call.
+    RCCL orders its transfers after the current stream itself, so nothing waits there."""
+    import torch.distributed as dist
+
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        torch.cuda.current_stream(t.device).synchronize()
+
+
 def exchange_interfaces(part: SlabPartition, values: torch.Tensor, slices: dict, groups, fixups=None,
                         diagonal: float = 1.0, async_op: bool = False, suffix: dict | None = None,
                         oneway: bool = False):
@@ -179,6 +189,7 @@ def exchange_interfaces(part: SlabPartition, values: torch.Tensor, slices: dict,
             idx = suffix[name]
             if name == "lower":
                 buf = flat.index_select(0, idx)
+                _host_staged_ready(buf, groups[q])
                 w = dist.isend(buf, dst=part.rank - 1, group=groups[q])
                 pending.append((w, None, buf, "send"))
             else:
@@ -194,6 +205,7 @@ def exchange_interfaces(part: SlabPartition, values: torch.Tensor, slices: dict,
             else:
                 b0, b1 = slices[name]
                 idx, buf = None, flat[b0:b1]
+            _host_staged_ready(buf, groups[q])
             w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=groups[q], async_op=True)
             pending.append((w, idx, buf, "copy"))
     handle = (pending, flat, values, fixups, diagonal)
@@ -247,6 +259,7 @@ def exchange_vector_interfaces(part: SlabPartition, b: torch.Tensor, bs: int, gr
     works = []
     for q, name in sorted(steps, key=lambda s: (s[0] % 2, s[0])):
         d0, d1 = rng[name]
+        _host_staged_ready(b, groups[q])
         works.append(dist.all_reduce(b[d0:d1], op=dist.ReduceOp.SUM, group=groups[q], async_op=async_op))
     if async_op:
         return works
