@@ -2469,6 +2469,27 @@ __device__ __forceinline__ void xchg_drain(double* acc, int h, int nv, double* o
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, hv), rv, (tid == 0 && h) ? 0 : OOB, 0, NTS);
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, tv), rv, (tid == 1 && tail) ? 8 * (nv - 1) : OOB, 0, NTS);
 }
+// An item's NBG slot words (u16) as packed pairs sl[t] = word 2t | word 2t+1 << 16. P2 simplices in
+// column halves (NN 10, NSPLIT 2: 20 B per entry, part p at byte 10 p): three aligned dword loads at
+// byte 8 p + {0, 4, 8}, shifted into place for the odd half (round 5; five u16 loads before: the
+// gathers' loads are bound by instructions through the texture path, not bytes)
+template <int NN, int NSPLIT, int NSL>
+__device__ __forceinline__ void load_slot_words(const uint16_t* __restrict__ slots, int64_t e, int part,
+                                                uint32_t (&sl)[NSL]) {
+  constexpr int NBG = NN / NSPLIT;
+  if constexpr (NN == 10 && NSPLIT == 2 && NSL == 3) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(slots + e * NN) + 2 * part;
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    sl[0] = part ? __builtin_amdgcn_alignbit(w1, w0, 16) : w0;
+    sl[1] = part ? __builtin_amdgcn_alignbit(w2, w1, 16) : w1;
+    sl[2] = part ? (w2 >> 16) : (w2 & 0xFFFFu);
+  } else {
+    const uint16_t* sp = slots + e * NN + part * NBG;
+#pragma unroll
+    for (int t = 0; t < NSL; ++t)
+      sl[t] = (uint32_t)sp[2 * t] | (2 * t + 1 < NBG ? (uint32_t)sp[2 * t + 1 < NBG ? 2 * t + 1 : 0] << 16 : 0u);
+  }
+}
 constexpr int FA_LIN_FUSE = 1;  // P1 simplices (fa_assemble_matrix): records formed inside k_gather_lin
 // 2^e for a normal exponent (|e| <= 1022), from its bits (no FP64 op: uniform e stays scalar)
 __device__ __forceinline__ double pow2(int e) { return __hiloint2double((e + 1023) << 20, 0); }
@@ -2594,10 +2615,7 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
       }
     }
     const int64_t e = d.a0 + min(jit, max(d.na - 1, 0));
-    const uint16_t* sp = P.slots + e * NN + part * NBG;
-#pragma unroll
-    for (int t = 0; t < (NBG + 1) / 2; ++t)
-      it.sl[t] = (uint32_t)sp[2 * t] | (2 * t + 1 < NBG ? (uint32_t)sp[2 * t + 1 < NBG ? 2 * t + 1 : 0] << 16 : 0u);
+    load_slot_words<NN, NSPLIT>(P.slots, e, part, it.sl);
     if constexpr (!FUSE) it.mask = rec_mask(it.r[GD * GD]);  // 0 without bcs (nothing was or-ed in)
   };
   // FUSE: the record (s Ji, sign of mu |J|) of the item's cell from its vertices (cell_record's
@@ -3199,9 +3217,7 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
         it.pt[ql][2 * k + 1] = v.y;
       }
     }
-    const uint16_t* sp = P.slots + entry_of(d) * NN + part * NBG;
-#pragma unroll
-    for (int t = 0; t < NSL; ++t) it.sl[t] = (uint32_t)sp[2 * t] | (2 * t + 1 < NBG ? (uint32_t)sp[2 * t + 1 < NBG ? 2 * t + 1 : 0] << 16 : 0u);
+    load_slot_words<NN, NSPLIT>(P.slots, entry_of(d), part, it.sl);
     it.mask = mk[c * mkmul] * mkmul;
   };
 
