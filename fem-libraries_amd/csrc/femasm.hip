@@ -1301,7 +1301,7 @@ static int launch_hex_mfma(int mode, const fa_mesh* mesh, const MeshView& M, con
 }
 
 // set bc diagonal entries (after the gather / scatter)
-template <int GD>
+template <int GD, int WPT>
 __global__ __launch_bounds__(256) void k_bc_diag(BsrView A, int64_t nnodes, const int8_t* __restrict__ bc, double diag,
                                                 int* err) {
   // dolfinx set_diagonal over the window's rows. A workgroup scans 64 KB of markers (16 aligned 16-B
@@ -1309,7 +1309,7 @@ __global__ __launch_bounds__(256) void k_bc_diag(BsrView A, int64_t nnodes, cons
   // resolves them (find_slot: ~7 dependent loads) on all its lanes at once. Round 5: a thread per dof
   // left about one active lane per wave, and config E's ~1 M constrained dofs of 202 M took 0.41 ms
   // (now 0.26).
-  constexpr int NT = 256, WPT = 16, QCAP = 4096;
+  constexpr int NT = 256, QCAP = 4096;
   constexpr int64_t SPAN = 16 * NT * WPT;
   __shared__ int64_t q[QCAP];
   __shared__ int qn;
@@ -1351,10 +1351,16 @@ __global__ __launch_bounds__(256) void k_bc_diag(BsrView A, int64_t nnodes, cons
     __syncthreads();  // the queue is read before the next pass resets it
   }
 }
-// k_bc_diag's grid for a window of n dofs (64 KB of markers per workgroup pass)
-static inline int bc_diag_grid(int64_t n) {
-  const int64_t g = (n + 16 + 65535) / 65536 + 1;
-  return (int)std::max<int64_t>(1, std::min<int64_t>(g, (1 << 24) - 8));
+// k_bc_diag over a window of n dofs: 64 KB of markers per workgroup pass, or 4 KB when that leaves
+// fewer than ~2,000 workgroups (config C's 5 M dofs: 80 workgroups of 64 KB resolved ~1,000 dofs each,
+// 0.068 ms; a thread per dof had taken 0.021 ms)
+template <int GD>
+static void launch_bc_diag(const BsrView& A, int64_t n, const int8_t* bc, double diag, int* err, hipStream_t s) {
+  auto grid = [](int64_t n, int64_t span) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>((n + 16 + span - 1) / span + 1, (1 << 24) - 8));
+  };
+  if (n >= 2048ll * 65536) k_bc_diag<GD, 16><<<grid(n, 65536), 256, 0, s>>>(A, 0, bc, diag, err);
+  else k_bc_diag<GD, 1><<<grid(n, 4096), 256, 0, s>>>(A, 0, bc, diag, err);
 }
 
 // ------------------------------------------------------------------------------------ gather kernel
@@ -4997,7 +5003,7 @@ static int launch_gather_neo(GatherArgs P, const int8_t* bc, hipStream_t s, cons
     LAUNCH_CHECK();
     HIP_TRY(hipFreeAsync(ldesc, s));
     if (bc) {  // Dirichlet diagonals (dolfinx set_diagonal) of the plan's rows
-      k_bc_diag<GD><<<bc_diag_grid((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
+      launch_bc_diag<GD>(P.A, (P.A.row_end - P.A.row_begin) * GD, bc, P.diag, P.err, s);
       LAUNCH_CHECK();
     }
   }
@@ -5080,7 +5086,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       LAUNCH_CHECK();
       HIP_TRY(hipFreeAsync(ldesc, s));
       if (bc) {
-        k_bc_diag<GD><<<bc_diag_grid((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
+        launch_bc_diag<GD>(P.A, (P.A.row_end - P.A.row_begin) * GD, bc, P.diag, P.err, s);
         LAUNCH_CHECK();
       }
       HIP_TRY(hipFreeAsync(xp, s));
@@ -5138,7 +5144,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
       LAUNCH_CHECK();
       HIP_TRY(hipFreeAsync(ldesc, s));
       if (bc) {  // Dirichlet diagonals (dolfinx set_diagonal) of the plan's rows
-        k_bc_diag<GD><<<bc_diag_grid((P.A.row_end - P.A.row_begin) * GD), 256, 0, s>>>(P.A, P.M.nnodes, bc, P.diag, P.err);
+        launch_bc_diag<GD>(P.A, (P.A.row_end - P.A.row_begin) * GD, bc, P.diag, P.err, s);
         LAUNCH_CHECK();
       }
       if (W.mode == GatherStage::FULL) {
@@ -5400,8 +5406,8 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     if (rc) return rc;
     if (bc) {
       int64_t n = (we - wb) * mesh->gdim;
-      if (mesh->gdim == 2) k_bc_diag<2><<<bc_diag_grid(n), 256, 0, s>>>(Av, mesh->nnodes, bc, diag, derr);
-      else k_bc_diag<3><<<bc_diag_grid(n), 256, 0, s>>>(Av, mesh->nnodes, bc, diag, derr);
+      if (mesh->gdim == 2) launch_bc_diag<2>(Av, n, bc, diag, derr, s);
+      else launch_bc_diag<3>(Av, n, bc, diag, derr, s);
       LAUNCH_CHECK();
     }
   }
