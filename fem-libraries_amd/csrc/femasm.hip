@@ -1466,6 +1466,8 @@ struct GatherArgs {
   const double* lat;  // MAT_AFFT: node lattice codes a0 + 8 a1 + 64 a2
   const double* rec;  // [ncells][Rec::SIZE]
   const uint32_t* bcmask;  // [ncells] or NULL
+  const uint32_t* cellmask; // fused P1 records with a dof numbering other than the geometry's: [ncells]
+                            // constrained-dof bits per cell (k_cell_bcmask), else NULL
   const double* xpack;      // fused P1 records (k_gather_lin FUSE): [nnodes][4] = the node's coordinates
                             // and its constrained-dof bits (as the bits of a double), k_pack_nodes
   int* err;
@@ -2610,7 +2612,7 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
         m |= (uint32_t)__double_as_longlong(GD == 3 ? b.y : b.x) << (t * GD);
       }
       it.E = P.F.E[c];
-      it.mask = m;
+      it.mask = P.cellmask ? P.cellmask[c] : m;  // (uniform branch)
     } else {
       const dv2* rp = reinterpret_cast<const dv2*>(P.rec + c * RL);
 #pragma unroll
@@ -4891,6 +4893,23 @@ struct GatherStage {
 };
 static inline int64_t align256(int64_t b) { return (b + 255) & ~int64_t(255); }
 
+// every cell's constrained-dof bits (bit t GD + j: dof j of its local node t, read by dof node), for
+// the fused P1 records of a dofmap other than the geometry's
+template <int GD, int NN>
+__global__ void k_cell_bcmask(const int32_t* __restrict__ cells, const int8_t* __restrict__ bc, int64_t ncells,
+                              uint32_t* __restrict__ out) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncells; c += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t m = 0u;
+#pragma unroll
+    for (int t = 0; t < NN; ++t) {
+      const int64_t n = cells[c * NN + t];
+#pragma unroll
+      for (int j = 0; j < GD; ++j) m |= (bc[n * GD + j] ? 1u : 0u) << (t * GD + j);
+    }
+    out[c] = m;
+  }
+}
+
 // every node's coordinates and constrained-dof bits (bit j: dof node * GD + j), for the fused P1 records
 template <int GD>
 __global__ void k_pack_nodes(const double* __restrict__ x, const int8_t* __restrict__ bc, int64_t nnodes,
@@ -5052,18 +5071,26 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   if constexpr (MAT == MAT_LINU && R::SIMP && NN == GD + 1 && NN % NSPLIT == 0 && FA_LIN_FUSE) {
     // P1 simplices through fa_assemble_matrix: k_gather_lin forms the records itself (FUSE)
     constexpr int LNT = lin_threads(GD, NN);
-    // (the fused items read their vertices' bc bits by geometry node: the same numbering as the
-    // dofmap's, which P1 shares -- another dofmap takes the records path below)
-    if (W.mode == GatherStage::FULL && P.nchunks > 0 && P.F.E && !P.cw && P.eadj && P.M.geom == P.M.cells &&
+    // (the node pack holds each vertex's bc bits when the dofmap is the geometry dofmap; with another
+    // P1 numbering the bits come per cell from k_cell_bcmask, read by dof node)
+    if (W.mode == GatherStage::FULL && P.nchunks > 0 && P.F.E && !P.cw && P.eadj &&
         P.slots && P.slot_order == NSPLIT && !P.corder && P.plan_maxadj * NSPLIT <= LNT && P.plan_maxadj >= 0 &&
         P.plan_maxb <= lin_maxb(GD, NN) && P.nchunks < (1ll << 31)) {
       int rc;
       double* xp = nullptr;
+      uint32_t* cm = nullptr;
+      const bool same = P.M.geom == P.M.cells;
       if ((rc = scratch_alloc((void**)&xp, sizeof(double) * 4 * (size_t)std::max<int64_t>(P.M.nnodes, 1), s))) return rc;
       if (P.M.nnodes > 0) {
-        k_pack_nodes<GD><<<grid_for(P.M.nnodes), 256, 0, s>>>(P.M.x, bc, P.M.nnodes, xp);
+        k_pack_nodes<GD><<<grid_for(P.M.nnodes), 256, 0, s>>>(P.M.x, same ? bc : nullptr, P.M.nnodes, xp);
         LAUNCH_CHECK();
       }
+      if (!same && bc && P.M.ncells > 0) {
+        if ((rc = scratch_alloc((void**)&cm, sizeof(uint32_t) * (size_t)P.M.ncells, s))) return rc;
+        k_cell_bcmask<GD, NN><<<grid_for(P.M.ncells), 256, 0, s>>>(P.M.cells, bc, P.M.ncells, cm);
+        LAUNCH_CHECK();
+      }
+      P.cellmask = cm;
       P.xpack = xp;
       P.bcmask = bc ? reinterpret_cast<const uint32_t*>(xp) : nullptr;  // only "has bcs" is read
       P.rec = nullptr;
@@ -5090,6 +5117,7 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
         LAUNCH_CHECK();
       }
       HIP_TRY(hipFreeAsync(xp, s));
+      if (cm) HIP_TRY(hipFreeAsync(cm, s));
       return FA_OK;
     }
   }
@@ -5377,7 +5405,7 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;
-    P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr; P.xpack = nullptr;
+    P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr; P.xpack = nullptr; P.cellmask = nullptr;
     P.affine = (plan->cell_flags & FA_PLAN_AFFINE) != 0;
     P.t1d = T.t1d; P.lat = T.lat;
     P.fix = ((flags & FA_DETERMINISTIC) || (plan->cell_flags & FA_PLAN_DETERMINISTIC)) ? 1 : 0;

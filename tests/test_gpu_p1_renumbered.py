@@ -1,9 +1,9 @@
 """P1 spaces whose node numbering is not the geometry's (FunctionSpace.from_dofmap: a permuted
-vertex numbering). The fused P1 gather reads each vertex's coordinates and bc bits by geometry node,
-so fa_assemble_matrix takes it only when the dofmap is the geometry dofmap; a renumbered space takes
-the records path, which reads the bc bits by dof node. The matrix of the renumbered space, permuted
-back, must equal the geometry-numbered one, bc rows, columns and diagonal included (round 5: before
-the guard the fused path marked the wrong rows)."""
+vertex numbering). The fused P1 gather reads each vertex's coordinates by geometry node; its bc bits
+come from the node pack when the dofmap is the geometry dofmap and per cell (k_cell_bcmask, read by
+dof node) otherwise. The matrix of the renumbered space, permuted back, must equal the
+geometry-numbered one, bc rows, columns and diagonal included (round 5: the round-4 fused path read
+the bits by geometry node and marked the wrong rows; this test fails on it)."""
 import numpy as np
 import pytest
 import torch
@@ -29,7 +29,7 @@ def test_renumbered_p1_space_equals_geometry_numbering(oracle, dev, ct, n):
     nv = V.num_nodes
     perm = torch.randperm(nv, generator=torch.Generator().manual_seed(7)).to(dev)
     V2 = fem.FunctionSpace.from_dofmap(m, 1, gd, perm[m.cells.to(torch.int64)], nv)
-    assert V2.dofmap.data_ptr() != m.cells.data_ptr()
+    assert V2.dofmap.data_ptr() != m.cells.data_ptr()  # the per-cell bc bits of the fused path
     E = torch.tensor(oracle.e_range()[np.arange(m.num_cells) % 200], device=dev)
     left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
     right = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.ones_like(x[0])))
