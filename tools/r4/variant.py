@@ -139,6 +139,15 @@ V = {
               "      constexpr int OOB = 0x40000000, NTS = 3;  // nt\n      // one descriptor over the chunk's nv values")],
     # P1 simplices through the records kernel + k_gather_lin (no fused records)
     "nofuse": [("constexpr int FA_LIN_FUSE = 1;", "constexpr int FA_LIN_FUSE = 0;")],
+    # k_gather_neo in 2-wave workgroups (128 items, chunks of <= 64 entries, 23 KB accumulator): 4
+    # workgroups per CU instead of 2 (round 4 measured 77.2 vs 75.9 ms with the previous drain)
+    "neo128": [("constexpr int FA_GATHER_LDS_NEO = 46080;", "constexpr int FA_GATHER_LDS_NEO = 23040;"),
+               ("__launch_bounds__(256, 2) void k_gather_neo(", "__launch_bounds__(128, 2) void k_gather_neo("),
+               ("  constexpr int NTH = 256;  // threads: 256 items", "  constexpr int NTH = 128;  // threads: 256 items"),
+               ("                             256 / neo_nsplit(mesh->cell_type, mesh->degree));",
+                "                             128 / neo_nsplit(mesh->cell_type, mesh->degree));"),
+               ("gather_grid(k_gather_neo<GD, NN, NQ, NSPLIT>, P.nchunks, 256);\n    k_gather_neo<GD, NN, NQ, NSPLIT><<<(unsigned)grid, 256, 0, s>>>",
+                "gather_grid(k_gather_neo<GD, NN, NQ, NSPLIT>, P.nchunks, 128);\n    k_gather_neo<GD, NN, NQ, NSPLIT><<<(unsigned)grid, 128, 0, s>>>")],
     # positional plans without the bank-balancing entry placement: position = adjacency order
     # (entries of a row, and of neighbouring rows, share cells: lanes of a quarter read nearby records)
     "perm_id": [("      const int j = gather_perm(jj, na, st, inv);\n      const int64_t e = a0 + j;\n      int64_t lo = r0, hi = r1 - 1;\n      while (lo < hi) {\n        const int64_t mid = (lo + hi + 1) >> 1;\n        if (adj_ptr[mid] <= e) lo = mid; else hi = mid - 1;\n      }\n      const int rowlo = (int)(indptr[lo] - b0);\n      uint8_t res[NN];",
