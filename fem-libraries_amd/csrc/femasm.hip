@@ -98,7 +98,7 @@ struct DevTables {
 constexpr int pk_width(int gd) { return gd == 3 ? 6 : 16; }
 constexpr int pk_low(int gd) { return gd == 3 ? 5 : 2; }
 static bool pack_ahat(int nn, int td, const std::vector<double>& ahat, std::vector<uint64_t>& pk, double& scale,
-                      double& nmax) {
+                      double& nmax, int* denom = nullptr) {
   if (td != 2 && td != 3) return false;
   const int w = pk_width(td), lo = pk_low(td), lim = (1 << (w - 1)) - 1;
   double amax = 0.0;
@@ -126,9 +126,26 @@ static bool pack_ahat(int nn, int td, const std::vector<double>& ahat, std::vect
         pk[t] |= e < lo ? f << (w * e) : f << (32 + w * (e - lo));
       }
     scale = 1.0 / std::sqrt((double)D);
+    if (denom) *denom = D;
     return true;
   }
   return false;
+}
+
+// Ahat[a][b][i][j] = sum_q w_q dphi_a(q)[i] dphi_b(q)[j] of a simplex element's rule
+static void simplex_ahat(const ElementTables& T, std::vector<double>& ah, double& amax) {
+  ah.clear();
+  amax = 0.0;
+  for (int a = 0; a < T.nn; ++a)
+    for (int b = 0; b < T.nn; ++b)
+      for (int i = 0; i < T.td; ++i)
+        for (int j = 0; j < T.td; ++j) {
+          double v = 0.0;
+          for (int q = 0; q < T.nq; ++q)
+            v += T.wq[q] * T.dphi[((size_t)q * T.nn + a) * T.td + i] * T.dphi[((size_t)q * T.nn + b) * T.td + j];
+          ah.push_back(v);
+          amax = std::max(amax, std::fabs(v));
+        }
 }
 
 static std::mutex g_tab_mu;
@@ -160,17 +177,8 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
   double amax = 0.0;
   std::vector<double> ah;
   if (is_simplex(ct)) {
-    for (int a = 0; a < T.nn; ++a)
-      for (int b = 0; b < T.nn; ++b)
-        for (int i = 0; i < T.td; ++i)
-          for (int j = 0; j < T.td; ++j) {
-            double v = 0.0;
-            for (int q = 0; q < T.nq; ++q)
-              v += T.wq[q] * T.dphi[((size_t)q * T.nn + a) * T.td + i] * T.dphi[((size_t)q * T.nn + b) * T.td + j];
-            h.push_back(v);
-            ah.push_back(v);
-            amax = std::max(amax, std::fabs(v));
-          }
+    simplex_ahat(T, ah, amax);
+    h.insert(h.end(), ah.begin(), ah.end());
   }
   std::vector<uint64_t> pk;
   double pk_scale = 0.0, pk_amax = 0.0;
@@ -236,6 +244,30 @@ extern "C" int fa_element_info(int32_t cell_type, int32_t degree, int32_t qdeg, 
   int qd = qdeg < 0 ? estimated_qdeg(cell_type, degree) : qdeg;
   if (nn) *nn = num_nodes(cell_type, degree);
   if (nq) *nq = make_quadrature(cell_type, qd).size();
+  return FA_OK;
+}
+
+// Host only (no device call): whether the element's reference tensor packs into the integer table the
+// P2 / P3 simplex gather reads (k_gather_lin), and its denominator D (Ahat = N / D); 0 = not packed
+// (the kernel then falls back to the generic gather).
+extern "C" int fa_element_table_info(int32_t cell_type, int32_t degree, int32_t qdeg, int32_t* packed_denom,
+                                     double* amax) {
+  if (!supported(cell_type, degree)) return fail(FA_E_UNSUPPORTED, "unsupported element: cell %d degree %d", cell_type, degree);
+  const int qd = qdeg < 0 ? estimated_qdeg(cell_type, degree) : qdeg;
+  if (qd > 12) return fail(FA_E_UNSUPPORTED, "quadrature degree %d > 12", qd);
+  int D = 0;
+  double am = 0.0;
+  if (is_simplex(cell_type)) {
+    ElementTables T;
+    if (!make_tables(cell_type, degree, qd, T)) return fail(FA_E_UNSUPPORTED, "element tables failed");
+    std::vector<double> ah;
+    simplex_ahat(T, ah, am);
+    std::vector<uint64_t> pk;
+    double sc = 0.0, nm = 0.0;
+    if (!pack_ahat(T.nn, T.td, ah, pk, sc, nm, &D)) D = 0;
+  }
+  if (packed_denom) *packed_denom = D;
+  if (amax) *amax = am;
   return FA_OK;
 }
 
@@ -1466,8 +1498,6 @@ struct GatherArgs {
   const double* lat;  // MAT_AFFT: node lattice codes a0 + 8 a1 + 64 a2
   const double* rec;  // [ncells][Rec::SIZE]
   const uint32_t* bcmask;  // [ncells] or NULL
-  const uint32_t* cellmask; // fused P1 records with a dof numbering other than the geometry's: [ncells]
-                            // constrained-dof bits per cell (k_cell_bcmask), else NULL
   const double* xpack;      // fused P1 records (k_gather_lin FUSE): [nnodes][4] = the node's coordinates
                             // and its constrained-dof bits (as the bits of a double), k_pack_nodes
   int* err;
@@ -1629,7 +1659,11 @@ __global__ __launch_bounds__(256) void k_cell_records_staged(MeshView M, FormVie
     const int nv = (int)min<int64_t>(64, M.ncells - cb) * R::SIZE;  // even
     const double2* s2 = reinterpret_cast<const double2*>(sb);
     double2* d2 = reinterpret_cast<double2*>(rec + cb * R::SIZE);
-    for (int t = lane; t < nv / 2; t += 64) d2[t] = s2[t];
+    for (int t = lane; t < nv / 2; t += 64) {
+      const fa_dv2 w = reinterpret_cast<const fa_dv2*>(s2)[t];
+      reinterpret_cast<fa_dv2*>(d2)[t] = w;
+      store_guard1(w);  // the next pass's LDS read returns into these registers
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2612,7 +2646,7 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
         m |= (uint32_t)__double_as_longlong(GD == 3 ? b.y : b.x) << (t * GD);
       }
       it.E = P.F.E[c];
-      it.mask = P.cellmask ? P.cellmask[c] : m;  // (uniform branch)
+      it.mask = m;
     } else {
       const dv2* rp = reinterpret_cast<const dv2*>(P.rec + c * RL);
 #pragma unroll
@@ -3848,8 +3882,11 @@ __global__ void k_check_hits(const uint8_t* __restrict__ hit, int64_t n, int* er
   if (e) atomicOr(err, e);
 }
 
-extern "C" int fa_check_pattern(const fa_mesh* mesh, const fa_adjacency* adj, const int64_t* indptr,
-                                const int32_t* indices, int64_t nblocks, void* stream) {
+// exact: also refuse a block no cell needs (bit 8: the pattern create_matrix builds). Assembling into
+// a superset pattern is valid (dolfinx / PETSc accept one: a rank's slab pattern, a pattern with room
+// for later entries), so fa_assemble_matrix's FA_CHECK_ERRORS checks without it.
+static int check_pattern(const fa_mesh* mesh, const fa_adjacency* adj, const int64_t* indptr,
+                         const int32_t* indices, int64_t nblocks, bool exact, void* stream) {
   int rc = check_mesh(mesh);
   if (rc) return rc;
   if (!adj || !adj->ptr || !adj->idx || !indptr || (!indices && nblocks > 0)) return fail(FA_E_ARG, "null argument");
@@ -3872,7 +3909,7 @@ extern "C" int fa_check_pattern(const fa_mesh* mesh, const fa_adjacency* adj, co
     k_check_pattern<<<grid_for(n), 256, 0, s>>>(M, adj->ptr, adj->idx, indptr, indices, nblocks, hit, derr);
     LAUNCH_CHECK();
   }
-  if (nblocks > 0) {
+  if (nblocks > 0 && exact) {
     k_check_hits<<<grid_for(nblocks), 256, 0, s>>>(hit, nblocks, derr);
     LAUNCH_CHECK();
   }
@@ -3892,6 +3929,11 @@ extern "C" int fa_check_pattern(const fa_mesh* mesh, const fa_adjacency* adj, co
                 (herr & 2) ? " columns out of range or unsorted" : "", (herr & 4) ? " a cell's (row, column) pair missing" : "",
                 (herr & 8) ? " a column no cell needs" : "", (herr & 32) ? " adjacency" : "");
   return FA_OK;
+}
+
+extern "C" int fa_check_pattern(const fa_mesh* mesh, const fa_adjacency* adj, const int64_t* indptr,
+                                const int32_t* indices, int64_t nblocks, void* stream) {
+  return check_pattern(mesh, adj, indptr, indices, nblocks, true, stream);
 }
 
 __global__ void k_build_slots(MeshView M, const int64_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj_idx,
@@ -4893,23 +4935,6 @@ struct GatherStage {
 };
 static inline int64_t align256(int64_t b) { return (b + 255) & ~int64_t(255); }
 
-// every cell's constrained-dof bits (bit t GD + j: dof j of its local node t, read by dof node), for
-// the fused P1 records of a dofmap other than the geometry's
-template <int GD, int NN>
-__global__ void k_cell_bcmask(const int32_t* __restrict__ cells, const int8_t* __restrict__ bc, int64_t ncells,
-                              uint32_t* __restrict__ out) {
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncells; c += (int64_t)gridDim.x * blockDim.x) {
-    uint32_t m = 0u;
-#pragma unroll
-    for (int t = 0; t < NN; ++t) {
-      const int64_t n = cells[c * NN + t];
-#pragma unroll
-      for (int j = 0; j < GD; ++j) m |= (bc[n * GD + j] ? 1u : 0u) << (t * GD + j);
-    }
-    out[c] = m;
-  }
-}
-
 // every node's coordinates and constrained-dof bits (bit j: dof node * GD + j), for the fused P1 records
 template <int GD>
 __global__ void k_pack_nodes(const double* __restrict__ x, const int8_t* __restrict__ bc, int64_t nnodes,
@@ -4935,12 +4960,16 @@ __global__ void k_pack_nodes(const double* __restrict__ x, const int8_t* __restr
 
 template <int GD>
 __global__ void k_bhat(const double* __restrict__ ahat, int nblk, double r, double* __restrict__ bhat) {
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nblk; t += gridDim.x * blockDim.x)
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nblk; t += gridDim.x * blockDim.x) {
+    double o[GD * GD];
 #pragma unroll
     for (int i = 0; i < GD; ++i)
 #pragma unroll
-      for (int k = 0; k < GD; ++k)
-        bhat[t * GD * GD + i * GD + k] = r * ahat[t * GD * GD + i * GD + k] + ahat[t * GD * GD + k * GD + i];
+      for (int k = 0; k < GD; ++k) o[i * GD + k] = r * ahat[t * GD * GD + i * GD + k] + ahat[t * GD * GD + k * GD + i];
+#pragma unroll
+    for (int e = 0; e < GD * GD; ++e) bhat[t * GD * GD + e] = o[e];
+    store_fence(o);
+  }
 }
 
 // k_gather_lin's constant operands: a zero mask word (no bcs) and a scratch line for the stores of
@@ -5071,26 +5100,20 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   if constexpr (MAT == MAT_LINU && R::SIMP && NN == GD + 1 && NN % NSPLIT == 0 && FA_LIN_FUSE) {
     // P1 simplices through fa_assemble_matrix: k_gather_lin forms the records itself (FUSE)
     constexpr int LNT = lin_threads(GD, NN);
-    // (the node pack holds each vertex's bc bits when the dofmap is the geometry dofmap; with another
-    // P1 numbering the bits come per cell from k_cell_bcmask, read by dof node)
-    if (W.mode == GatherStage::FULL && P.nchunks > 0 && P.F.E && !P.cw && P.eadj &&
+    // Only when the dofmap IS the geometry dofmap: the pack is indexed by vertex id and built over the
+    // space's nodes, which are then the vertices (num_nodes == num_vertices). A space with its own P1
+    // numbering (FunctionSpace.from_dofmap, a rank's slab) may have more or fewer nodes than the mesh
+    // has vertices: it assembles through the records kernel (bc bits read by dof node, cell_bcmask).
+    if (W.mode == GatherStage::FULL && P.nchunks > 0 && P.F.E && !P.cw && P.eadj && P.M.geom == P.M.cells &&
         P.slots && P.slot_order == NSPLIT && !P.corder && P.plan_maxadj * NSPLIT <= LNT && P.plan_maxadj >= 0 &&
         P.plan_maxb <= lin_maxb(GD, NN) && P.nchunks < (1ll << 31)) {
       int rc;
       double* xp = nullptr;
-      uint32_t* cm = nullptr;
-      const bool same = P.M.geom == P.M.cells;
       if ((rc = scratch_alloc((void**)&xp, sizeof(double) * 4 * (size_t)std::max<int64_t>(P.M.nnodes, 1), s))) return rc;
       if (P.M.nnodes > 0) {
-        k_pack_nodes<GD><<<grid_for(P.M.nnodes), 256, 0, s>>>(P.M.x, same ? bc : nullptr, P.M.nnodes, xp);
+        k_pack_nodes<GD><<<grid_for(P.M.nnodes), 256, 0, s>>>(P.M.x, bc, P.M.nnodes, xp);
         LAUNCH_CHECK();
       }
-      if (!same && bc && P.M.ncells > 0) {
-        if ((rc = scratch_alloc((void**)&cm, sizeof(uint32_t) * (size_t)P.M.ncells, s))) return rc;
-        k_cell_bcmask<GD, NN><<<grid_for(P.M.ncells), 256, 0, s>>>(P.M.cells, bc, P.M.ncells, cm);
-        LAUNCH_CHECK();
-      }
-      P.cellmask = cm;
       P.xpack = xp;
       P.bcmask = bc ? reinterpret_cast<const uint32_t*>(xp) : nullptr;  // only "has bcs" is read
       P.rec = nullptr;
@@ -5117,7 +5140,6 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
         LAUNCH_CHECK();
       }
       HIP_TRY(hipFreeAsync(xp, s));
-      if (cm) HIP_TRY(hipFreeAsync(cm, s));
       return FA_OK;
     }
   }
@@ -5384,9 +5406,10 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
   DevTables T;
   if ((rc = get_tables(mesh->cell_type, mesh->degree, form->qdeg, &T))) return rc;
   hipStream_t s = (hipStream_t)stream;
-  // FA_CHECK_ERRORS: the pattern and adjacency are validated on the device first (fa_check_pattern)
+  // FA_CHECK_ERRORS: the pattern and adjacency are validated on the device first (fa_check_pattern
+  // without its exactness bit: a superset pattern assembles correctly)
   if ((flags & FA_CHECK_ERRORS) && adj && adj->ptr && adj->idx &&
-      (rc = fa_check_pattern(mesh, adj, A->indptr, A->indices, A->nblocks, stream)))
+      (rc = check_pattern(mesh, adj, A->indptr, A->indices, A->nblocks, false, stream)))
     return rc;
   MeshView M{mesh->cells, mesh->geom, mesh->x, mesh->ncells, mesh->nnodes, mesh->nn, mesh->nv, mesh->gdim};
   BsrView Av{A->indptr, A->indices, A->data, wb, we};
@@ -5405,7 +5428,7 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;
-    P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr; P.xpack = nullptr; P.cellmask = nullptr;
+    P.bc = bc; P.diag = diag; P.tab = T.wq; P.ahat = T.ahat; P.rec = nullptr; P.bcmask = nullptr; P.err = derr; P.xpack = nullptr;
     P.affine = (plan->cell_flags & FA_PLAN_AFFINE) != 0;
     P.t1d = T.t1d; P.lat = T.lat;
     P.fix = ((flags & FA_DETERMINISTIC) || (plan->cell_flags & FA_PLAN_DETERMINISTIC)) ? 1 : 0;
@@ -5682,8 +5705,12 @@ __global__ __launch_bounds__(256) void k_vector(MeshView M, FormView F, DevTable
         }
       }
     }
+    double o[GD];
 #pragma unroll
-    for (int i = 0; i < GD; ++i) b[a * GD + i] += r[i];
+    for (int i = 0; i < GD; ++i) o[i] = b[a * GD + i] + r[i];
+#pragma unroll
+    for (int i = 0; i < GD; ++i) b[a * GD + i] = o[i];
+    store_fence(o);  // the grid-stride loop's next node would rewrite the store's data registers
   }
 }
 
@@ -5771,8 +5798,12 @@ __global__ __launch_bounds__(256) void k_lifting(MeshView M, FormView F, DevTabl
         }
       }
     }
+    double o[GD];
 #pragma unroll
-    for (int i = 0; i < GD; ++i) b[a * GD + i] -= alpha * r[i];
+    for (int i = 0; i < GD; ++i) o[i] = b[a * GD + i] - alpha * r[i];
+#pragma unroll
+    for (int i = 0; i < GD; ++i) b[a * GD + i] = o[i];
+    store_fence(o);  // (as k_vector)
   }
 }
 

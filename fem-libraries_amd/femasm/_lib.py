@@ -94,6 +94,7 @@ SIGNATURES = {
     "fa_last_error": (ctypes.c_char_p, []),
     "fa_version": (ctypes.c_int, []),
     "fa_element_info": (ctypes.c_int, [I32, I32, I32, P, P]),
+    "fa_element_table_info": (ctypes.c_int, [I32, I32, I32, P, P]),
     "fa_build_adjacency": (ctypes.c_int, [P, P, P, P]),
     "fa_sparsity_count": (ctypes.c_int, [P, P, P, P, P]),
     "fa_sparsity_fill": (ctypes.c_int, [P, P, P, P, P]),

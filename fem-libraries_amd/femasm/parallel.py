@@ -372,14 +372,15 @@ class SlabProblem:
                                            if exchange == "oneway" else "a 2-rank all_reduce(SUM)")
                             + ", overlapping the interior rows")
 
-    def assemble(self, overlap: bool = True):
+    def assemble(self, overlap: bool = True, check: bool = False):
         """Records of all cells; the interface-plane rows; their 2-rank all-reduces issued on
         RCCL's stream; the interior rows on the compute stream meanwhile; wait; bc diagonals.
-        (ghost mode: one gather over the owned rows, nothing exchanged.)"""
+        (ghost mode: one gather over the owned rows, nothing exchanged.) check (ghost mode):
+        FA_CHECK_ERRORS -- the slab's pattern is a superset of its assembled cells' pairs."""
         if self.mode == "ghost":
             from . import fem
 
-            fem.assemble_matrix(self.a, bcs=self.bcs, A=self.A)
+            fem.assemble_matrix(self.a, bcs=self.bcs, A=self.A, check=check)
             return
         sg = self.split
         sg.prepare()

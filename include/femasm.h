@@ -164,6 +164,12 @@ int fa_version(void);
 /* Element metadata: nodes per cell and quadrature points for (cell_type, degree, qdeg). */
 int fa_element_info(int32_t cell_type, int32_t degree, int32_t qdeg, int32_t* nn, int32_t* nq);
 
+/* Host-only (no device call): whether a simplex element's reference tensor Ahat (default rule for
+ * qdeg < 0) is exactly N / D with small integers, i.e. packs into the integer table the P2 / P3 simplex
+ * gather reads; *packed_denom = D, or 0 when it does not pack (that element then assembles through the
+ * generic gather) or for tensor cells. *amax = max |Ahat| (simplices). Either pointer may be NULL. */
+int fa_element_table_info(int32_t cell_type, int32_t degree, int32_t qdeg, int32_t* packed_denom, double* amax);
+
 /* Node -> cell adjacency (transpose of the dofmap): ptr [nnodes+1], idx [ncells*nn]. */
 int fa_build_adjacency(const fa_mesh* mesh, int64_t* ptr, int32_t* idx, void* stream);
 

@@ -24,6 +24,20 @@ def _port():
     return p
 
 
+def _cfg(kind):
+    import bench
+
+    return bench.CONFIGS[{"neo": "Eneo", "p1": "C"}.get(kind, "E")]
+
+
+def _slab(n, rank, world, dev, kind, **kw):
+    from femasm import parallel
+
+    if kind == "p1":  # P1 tetrahedra: the slab's own node numbering (from_dofmap), not the mesh's vertices
+        return parallel.SlabProblem(n, rank, world, dev, degree=1, **kw)
+    return parallel.SlabProblem(n, rank, world, dev, form=kind, **kw)
+
+
 def _worker(rank, world, port, n, kind="linear"):
     import sys
 
@@ -37,10 +51,10 @@ def _worker(rank, world, port, n, kind="linear"):
     import rowparity
 
     dev = torch.device("cuda", 0)
-    prob = parallel.SlabProblem(n, rank, world, dev, form=kind)
+    prob = _slab(n, rank, world, dev, kind)
     prob.assemble()
     torch.cuda.synchronize()
-    m, V, a, bcs = bench.build_problem(n, dev, cfg=bench.CONFIGS["Eneo" if kind == "neo" else "E"])
+    m, V, a, bcs = bench.build_problem(n, dev, cfg=_cfg(kind))
     A = fem.assemble_matrix(a, bcs=bcs)
     part = prob.part
     ip_l = prob.A.indptr.cpu().numpy()
@@ -69,7 +83,7 @@ def _worker(rank, world, port, n, kind="linear"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n,kind", [(2, 6, "linear"), (3, 7, "linear"), (2, 6, "neo")])
+@pytest.mark.parametrize("world,n,kind", [(2, 6, "linear"), (3, 7, "linear"), (2, 6, "neo"), (3, 7, "p1")])
 def test_slab_problem_gpu_gloo(world, n, kind):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -119,11 +133,14 @@ def test_slab_residual_gpu_gloo(world, n, kind):
     mp.spawn(_residual_worker, args=(world, _port(), n, kind), nprocs=world, join=True)
 
 
-@pytest.mark.parametrize("world,n,kind", [(2, 6, "linear"), (3, 7, "neo")])
+@pytest.mark.parametrize("world,n,kind", [(2, 6, "linear"), (3, 7, "neo"), (3, 7, "p1")])
 def test_slab_ghost_mode_gpu(world, n, kind):
     """SlabProblem(mode="ghost"): no exchange; each rank's owned rows (HIP gather over its slab plus
     the layer above) equal the single-process full-mesh GPU assembly. The ranks need no
-    communication, so they run one after the other in this process."""
+    communication, so they run one after the other in this process. The assembly runs with
+    FA_CHECK_ERRORS: the slab pattern (built over the ghost layers too) is a superset of the pairs
+    of the cells it assembles, which the check must accept. P1 ("p1"): the slab's node numbering
+    differs from its mesh's vertex numbering, and ranks > 0 have more nodes than vertices."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import sys
@@ -136,12 +153,12 @@ def test_slab_ghost_mode_gpu(world, n, kind):
     import rowparity
 
     dev = torch.device("cuda", 0)
-    m, V, a, bcs = bench.build_problem(n, dev, cfg=bench.CONFIGS["Eneo" if kind == "neo" else "E"])
+    m, V, a, bcs = bench.build_problem(n, dev, cfg=_cfg(kind))
     A = fem.assemble_matrix(a, bcs=bcs)
     ip_g, ix_g, vg = A.indptr.cpu().numpy(), A.indices.cpu().numpy(), A.data.cpu().numpy()
     for rank in range(world):
-        prob = parallel.SlabProblem(n, rank, world, dev, form=kind, mode="ghost")
-        prob.assemble()
+        prob = _slab(n, rank, world, dev, kind, mode="ghost")
+        prob.assemble(check=True)
         torch.cuda.synchronize()
         part = prob.part
         r0, r1 = part.owned_rows

@@ -55,6 +55,43 @@ FAKE = """
 """
 
 
+# control flow (addresses as llvm-objdump prints them): a writer behind a TAKEN branch is a site; a
+# writer past an unconditional branch (never executed next) is not; a loop's back edge brings the loop
+# head's writers after a store at the bottom of the loop
+FAKE_CF = """
+0000000000001000 <_Z6k_takenv>:
+\tbuffer_store_dwordx4 v[10:13], v1, s[4:7], 0 offen  // 000000001000: E07C0000 80010A01
+\ts_cbranch_scc1 2  // 000000001008: BF850002
+\tv_mov_b32_e32 v40, 0  // 00000000100C: 7E500280
+\ts_endpgm  // 000000001010: BF810000
+\tv_mov_b32_e32 v41, 0  // 000000001014: 7E520280
+\tv_mov_b32_e32 v11, 0  // 000000001018: 7E160280
+\ts_endpgm  // 00000000101C: BF810000
+0000000000002000 <_Z7k_skipsv>:
+\tbuffer_store_dwordx4 v[10:13], v1, s[4:7], 0 offen  // 000000002000: E07C0000 80010A01
+\ts_branch 1  // 000000002008: BF820001
+\tv_mov_b32_e32 v12, 0  // 00000000200C: 7E180280
+\ts_nop 7  // 000000002010: BF800007
+\ts_nop 7  // 000000002014: BF800007
+\tv_mov_b32_e32 v12, 0  // 000000002018: 7E180280
+\ts_endpgm  // 00000000201C: BF810000
+0000000000003000 <_Z6k_loopv>:
+\tv_mov_b32_e32 v20, 0  // 000000003000: 7E280280
+\tv_add_u32_e32 v1, 16, v1  // 000000003004: 68020290
+\tbuffer_store_dwordx4 v[20:23], v1, s[4:7], 0 offen  // 000000003008: E07C0000 80011401
+\ts_cbranch_vccnz 65531  // 000000003010: BF87FFFB
+\ts_endpgm  // 000000003014: BF810000
+"""
+
+
+def test_checker_follows_branches():
+    sites = {s[0]: s for s in SH.check(FAKE_CF)}
+    assert "_Z6k_takenv" in sites and sites["_Z6k_takenv"][2].startswith("v_mov_b32_e32 v11")
+    assert sites["_Z6k_takenv"][3] == 3  # branch (1), v41 (2), v11 (3) on the taken path
+    assert "_Z7k_skipsv" not in sites  # the first v12 write is jumped over; the second is 16 wait states on
+    assert "_Z6k_loopv" in sites and sites["_Z6k_loopv"][2].startswith("v_mov_b32_e32 v20")
+
+
 def test_checker_finds_known_patterns():
     """The checker itself: a write 3 wait states after the store is a site; 16 wait states of
     s_nop, a vmcnt(0) wait, an LDS write's address operand and an unrelated load are not; an LDS

@@ -7,7 +7,9 @@ record kernels (`store_fence`). This checker disassembles the gfx950 code object
 libfemasm.so and reports every 12- or 16-byte vector-memory store (buffer / global / flat /
 scratch `_dwordx3` / `_dwordx4`) whose data VGPRs an instruction writes within WINDOW instructions
 after it (counted in wait states: one per instruction, k + 1 for `s_nop k`), with no
-`s_waitcnt vmcnt(0)` or `s_barrier` in between.
+`s_waitcnt vmcnt(0)` or `s_barrier` in between, on any control-flow path: `s_branch` continues at
+its target, `s_cbranch_*` at its target and at the next instruction (round 6; the round-5 checker
+followed address order only).
 
 Exempt (reported, not failed): scratch stores (the compiler's own register spills), rocPRIM's
 kernels (third-party, used by the sparsity build, whose pattern fa_check_pattern validates) and the
@@ -82,11 +84,13 @@ def store_data(op: str, ops):
     return vregs(ops[1]) if len(ops) > 1 else None
 
 
-def check(text: str, window: int = WINDOW):
-    """[(function, store line, writer line, distance)] of every hazard site."""
-    sites = []
+_ADDR = re.compile(r"//\s*([0-9A-Fa-f]+):")
+
+
+def parse(text: str):
+    """[(fn, op, ops, line, address or None)] in address order."""
     fn = None
-    insts = []  # (fn, op, ops, line)
+    insts = []
     for line in text.splitlines():
         m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
         if m:
@@ -96,26 +100,68 @@ def check(text: str, window: int = WINDOW):
         if not s or s.startswith(";") or fn is None or not line.startswith("\t"):
             continue
         parts = s.split(None, 1)
-        insts.append((fn, parts[0], _operands(parts[1]) if len(parts) > 1 else [], s.split("//")[0].strip()))
-    for i, (f, op, ops, ln) in enumerate(insts):
+        a = _ADDR.search(s)
+        insts.append((fn, parts[0], _operands(parts[1]) if len(parts) > 1 else [], s.split("//")[0].strip(),
+                      int(a.group(1), 16) if a else None))
+    return insts
+
+
+def successors(insts, at, j):
+    """Indices that can execute after instruction j (control flow: s_branch goes to its target only,
+    s_cbranch_* to its target and the next instruction; s_endpgm / s_setpc end the path). A branch
+    target is the instruction at address + 4 + 4 * simm16 (SOPP); without addresses (or a target
+    outside the function) a branch is followed by the next instruction only."""
+    f, op, ops, _, addr = insts[j]
+    nxt = [j + 1] if j + 1 < len(insts) and insts[j + 1][0] == f else []
+    if op in ("s_endpgm", "s_setpc_b64", "s_endpgm_saved"):
+        return []
+    if op == "s_branch" or op.startswith("s_cbranch_"):
+        tgt = None
+        if addr is not None and ops:
+            try:
+                k = int(ops[0].split()[0], 0)
+                k = k - 65536 if k >= 32768 else k
+                tgt = at.get((f, addr + 4 + 4 * k))
+            except ValueError:
+                tgt = None
+        if tgt is None:
+            return nxt
+        return [tgt] if op == "s_branch" else sorted(set(nxt + [tgt]))
+    return nxt
+
+
+def check(text: str, window: int = WINDOW):
+    """[(function, store line, writer line, distance)] of every hazard site: from each 12/16-B store,
+    every control-flow path (successors()) is walked for `window` wait states; the first write of a
+    data VGPR on any path is a site, a path ends at s_barrier, s_endpgm or s_waitcnt vmcnt(0)."""
+    sites = []
+    insts = parse(text)
+    at = {(f, a): k for k, (f, _, _, _, a) in enumerate(insts) if a is not None}
+    for i, (f, op, ops, ln, _) in enumerate(insts):
         if not _STORE.match(op):
             continue
         data = store_data(op, ops)
         if not data:
             continue
-        ws = 0
-        for d in range(1, 4 * window + 1):
-            if i + d >= len(insts) or insts[i + d][0] != f:
-                break
-            f2, op2, ops2, ln2 = insts[i + d]
+        best = {}  # instruction index -> fewest wait states it is reached with
+        work = [(j, 0) for j in successors(insts, at, i)]
+        hit = None
+        while work:
+            j, ws = work.pop()
+            if ws >= window or best.get(j, window) <= ws:
+                continue
+            best[j] = ws
+            f2, op2, ops2, ln2, _ = insts[j]
             if op2 == "s_barrier" or op2 == "s_endpgm" or (op2 == "s_waitcnt" and "vmcnt(0)" in " ".join(ops2)):
-                break
+                continue
             if dest_vgprs(op2, ops2) & data:
-                sites.append((f, ln, ln2, ws + 1))
-                break
-            ws += int(ops2[0], 0) + 1 if op2 == "s_nop" and ops2 else 1
-            if ws >= window:
-                break
+                if hit is None or ws + 1 < hit[1]:
+                    hit = (ln2, ws + 1)
+                continue
+            step = int(ops2[0], 0) + 1 if op2 == "s_nop" and ops2 else 1
+            work.extend((k, ws + step) for k in successors(insts, at, j))
+        if hit:
+            sites.append((f, ln, hit[0], hit[1]))
     return sites
 
 
