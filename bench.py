@@ -319,6 +319,42 @@ def time_steps(step, steps: int, warmup: int, dev, dist=None):
     return time.perf_counter() - t_start, float(np.mean([s.elapsed_time(e) for s, e in evs]))
 
 
+def slab_leg(parallel, n: int, rank: int, world: int, dev, args, mode: str, dist) -> dict:
+    """N > 1: build this rank's slab in one mode ("exchange": interface rows first, then a one-way RCCL
+    send of the upper rank's interface blocks to the owner overlapping the interior rows -- the
+    reference's PETSc stash, FEniCSx/mechanic2d/asym_elasto_damage_model.cc:853-854; "ghost": the layer
+    above the slab assembled redundantly, no exchange), time K steps (barrier + synchronize on both
+    sides, max over ranks), free it. Both modes leave every rank's owned rows complete."""
+    t0 = time.time()
+    prob = parallel.SlabProblem(n, rank, world, dev, form="neo" if args.config == "Eneo" else "linear", mode=mode)
+    prob.plan()
+    torch.cuda.synchronize()
+    setup = time.time() - t0
+
+    def step():
+        prob.assemble(overlap=not args.no_overlap)
+    elapsed, launch_ms = time_steps(step, args.steps, args.warmup, dev, dist)
+    t = torch.tensor([elapsed, launch_ms, setup], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, launch_ms, setup = float(t[0]), float(t[1]), float(t[2])
+    tot = torch.tensor([prob.num_cells, prob.num_cells_assembled, prob.exchange_bytes, prob.exchange_bytes],
+                       dtype=torch.int64, device=dev)
+    mx = tot[3:].clone()
+    dist.all_reduce(tot)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    ms = elapsed / args.steps * 1e3
+    comp = compulsory_bytes(prob.V, prob.A, prob.num_cells, True, state=args.config == "Eneo")
+    out = {"ms_per_step": round(ms, 4), "launch_ms": round(launch_ms, 4),
+           "value": round(int(tot[0]) / (ms * 1e-3) / 1e6, 3), "unit": "Melements/s", "cells": int(tot[0]),
+           "cells_assembled": int(tot[1]), "exchange_MB_total": round(int(tot[2]) / 1e6, 1),
+           "exchange_MB_max": round(int(mx[0]) / 1e6, 1), "setup_s": round(setup, 2),
+           "what": prob.kernel_name, "_ncells_local": prob.num_cells, "_comp": comp}
+    del prob, step
+    torch.cuda.empty_cache()
+    dist.barrier()
+    return out
+
+
 def eneo_block(dev, steps: int, warmup: int) -> dict:
     """Config E as BASELINE.json states its physics: the neo-Hookean AD tangent on the same 50.2 M-cell
     P2 mesh, timed in this process after the linear problem is freed (secondary block of the default
@@ -375,12 +411,12 @@ def main():
     ap.add_argument("--cpu-reps", type=int, default=7)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true", help="N > 1: exchange after all rows (no overlap)")
-    ap.add_argument("--slab-mode", default="ghost", choices=["exchange", "ghost"],
-                    help="N > 1: the communication-free redundant ghost layer (default, SURVEY §8(e) alternative) "
-                         "or the RCCL interface exchange. Ghost is the default since round 5: on one GPU a transfer "
-                         "paced to an xGMI link beside the interior rows was starved of CUs by the persistent gather "
-                         "(rank 3 of 8: interior + transfer 6.24 ms against a 4.78 ms ghost-mode slab; "
-                         "profiles/r5/overlap_*.json, DESIGN.md §7)")
+    ap.add_argument("--slab-mode", default="both", choices=["both", "exchange", "ghost"],
+                    help="N > 1: 'both' (default) times the RCCL interface exchange (the reference's PETSc-stash "
+                         "semantics, north-star path) AND the communication-free redundant ghost layer (SURVEY §8(e) "
+                         "alternative) one after the other in this run, each a complete assembly of every rank's "
+                         "owned rows; the headline value is the faster leg and the line carries both ('legs'). "
+                         "'exchange' / 'ghost' time one mode only")
     ap.add_argument("--no-hbm-probe", action="store_true", help="skip the measured-HBM-peak stream probe")
     ap.add_argument("--plan-search", action="store_true",
                     help="plan the LDS order with the alternating-path search (FA_PLAN_ORDER_SEARCH: ~10x plan time)")
@@ -444,18 +480,25 @@ def main():
             log(f"[bench] HBM probe failed: {e}")
     t0 = time.time()
     t_pattern = t_plan = 0.0
+    legs, best = None, None
     if world > 1:
         from femasm import parallel
 
         if args.config not in ("E", "Eneo"):
             raise SystemExit("N > 1 shards config E's mesh (P2 tets; linear elasticity or neo-Hookean) only")
-        prob = parallel.SlabProblem(n, rank, world, dev, form="neo" if args.config == "Eneo" else "linear",
-                                    mode=args.slab_mode)
-
-        def step():
-            prob.assemble(overlap=not args.no_overlap)
-        ncells_local = prob.num_cells
-        V_loc, A_loc, with_bc = prob.V, prob.A, True
+        legs = {}
+        modes = ["exchange", "ghost"] if args.slab_mode == "both" else [args.slab_mode]
+        for mode in modes:
+            legs[mode] = slab_leg(parallel, n, rank, world, dev, args, mode, dist)
+            log(f"[bench] slab mode {mode}: {legs[mode]['ms_per_step']:.3f} ms per step (max over ranks)")
+        best = min(legs, key=lambda k: legs[k]["ms_per_step"])
+        L = legs[best]
+        ncells_local, comp_leg = L.pop("_ncells_local"), L.pop("_comp")
+        for other in legs.values():
+            other.pop("_ncells_local", None)
+            other.pop("_comp", None)
+        elapsed, launch_ms, ncells_total = L["ms_per_step"] * args.steps * 1e-3, L["launch_ms"], L["cells"]
+        exchange_mb = L["exchange_MB_max"]
     else:
         m, V, a, bcs = build_problem(n, dev, cfg=cfg)
         torch.cuda.synchronize()
@@ -475,31 +518,22 @@ def main():
             fem.assemble_matrix(a, bcs=bcs, A=A, method=args.method, deterministic=args.deterministic,
                                 plan={"search": True} if args.plan_search else None)
 
-    torch.cuda.synchronize()
-    setup_s = time.time() - t0
+        torch.cuda.synchronize()
+    setup_s = time.time() - t0 if legs is None else legs[best]["setup_s"]
     log(f"[bench] setup {setup_s:.1f}s (pattern {t_pattern:.1f}s, plan {t_plan:.1f}s): {ncells_local} cells "
         f"on rank {rank}")
 
-    # per-launch kernel durations: HIP events on the launch stream (torch's current stream)
-    elapsed, launch_ms = time_steps(step, args.steps, args.warmup, dev, dist)
-    if dist is not None:
-        t = torch.tensor([elapsed, launch_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, launch_ms = float(t[0]), float(t[1])
-        tot = torch.tensor([ncells_local], dtype=torch.int64, device=dev)
-        dist.all_reduce(tot)
-        ncells_total = int(tot[0])
-        xb = torch.tensor([prob.exchange_bytes], dtype=torch.int64, device=dev)
-        dist.all_reduce(xb, op=dist.ReduceOp.MAX)
-        exchange_mb = round(int(xb[0]) / 1e6, 1)
-    else:
+    if legs is None:
+        # per-launch kernel durations: HIP events on the launch stream (torch's current stream)
+        elapsed, launch_ms = time_steps(step, args.steps, args.warmup, dev, dist)
         ncells_total = ncells_local
 
     ms_per_step = elapsed / args.steps * 1e3
     melem_s = ncells_total / (ms_per_step * 1e-3) / 1e6
     # roofline.achieved: the algorithmic (write-once, compulsory) bytes of this rank's assembly over
     # the live event time of one launch on the launch stream
-    comp = compulsory_bytes(V_loc, A_loc, ncells_local, with_bc, state=cfg.get("form") == "neo")
+    comp = comp_leg if legs is not None else \
+        compulsory_bytes(V_loc, A_loc, ncells_local, with_bc, state=cfg.get("form") == "neo")
     achieved = comp["total"] / (launch_ms * 1e-3) / 1e9
     # traffic: PMC-measured HBM bytes per launch of this build (profiles/traffic.json, keyed on the
     # femasm.hip hash), with its own fraction of peak; the SURVEY §8(d) element-stream model B_e is
@@ -611,10 +645,12 @@ def main():
                                         f"{'RCCL' if backend == 'nccl' else backend} send of the upper rank's "
                                         f"plane blocks to the owner ({exchange_mb} MB max sent per rank) "
                                         f"{'after' if args.no_overlap else 'overlapping'} the interior rows")
-                                       if args.slab_mode == "exchange" else
+                                       if best == "exchange" else
                                        f"z-slabs x{world}, no exchange: each rank also assembles the cell layer "
                                        f"above its slab (redundant ghost layer) so its owned rows are complete")
+                       + (f"; the faster of the legs {sorted(legs)} (both in 'legs')" if len(legs) > 1 else "")
                        if world > 1 else "single GPU"},
+            "legs": legs,
             # per GPU (rank 0 / slowest rank): achieved = algorithmic bytes of the assembly / launch time
             "roofline": {"bound": "fp64_valu" if compute_bound else "hbm",
                          "achieved": round(tflops_exec, 3) if compute_bound else round(achieved, 1),

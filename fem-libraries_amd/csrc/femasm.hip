@@ -2564,7 +2564,9 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
   // the reference tensor, one packed integer block per (a, b) (pk_ahat: Ahat_ab = N_ab / D; the item
   // records are scaled by 1 / sqrt(D)); P1 simplices use none
   __shared__ uint64_t tab[P1G ? 1 : NN * NN];
-  __shared__ uint32_t s_fx[2];  // FIX: scale exponent of the chunks of each parity (max over their items)
+  // FIX: per-block scale exponents of the chunks of each parity ([parity][chunk-relative block]: max
+  // over the items adding into the block), round 6 (round 4-5: one exponent per chunk)
+  __shared__ uint32_t s_bx[FIX ? 2 * MAXB : 1];
   constexpr int LOOK = FUSE ? 4 : 3;  // chunk descriptors in flight (d0 .. d[LOOK-1])
   constexpr int AHEAD = LOOK + 2;     // chunk ids fetched ahead of the chunk being gathered
   constexpr int RING = 8;
@@ -2591,7 +2593,8 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
   if constexpr (!P1G)
     for (int t = tid; t < NN * NN; t += NT) tab[t] = P.pk[t];
   for (int t = tid; t < NP2; t += NT) acc2[t] = dv2{0.0, 0.0};
-  if (tid < 2) s_fx[tid] = 0u;
+  if constexpr (FIX)
+    for (int t = tid; t < 2 * MAXB; t += NT) s_bx[t] = 0u;
 
   const int32_t* __restrict__ eadj = P.eadj;
   // a chunk: first block and adjacency entry, block and entry counts (< 2^31 each: fa_plan_gather's caps);
@@ -2684,13 +2687,16 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
       it.r[GD * GD] = s2 < 0.0 ? -1.0 : 1.0;
     }
   };
-  // FIX (deterministic mode): every contribution v of chunk k is added as the integer
-  // round(v * 2^se_k) with ds_add_u64, so a block's sum is exact and independent of the order of
-  // the adds; the drain converts it back (one rounding). se_k = 1072 - e_k with e_k the largest
-  // biased exponent of the chunk's item bounds fixc * rho^2 >= |block entry|, so |v * 2^se| < 2^50
-  // (the 1.5 * 2^52 rounding constant below is exact there) and up to 2^13 contributions never
-  // overflow. The chunk's e_k is the max over its items (per wave by DPP, then one ds_max_u32 per
-  // wave into s_fx[k & 1]), formed at the end of chunk k-1 from its prefetched items.
+  // FIX (deterministic mode): every contribution v to block b of chunk k is added as the integer
+  // round(v * 2^se_b) with ds_add_u64, so a block's sum is exact and independent of the order of
+  // the adds; the drain converts it back (one rounding). se_b = 1072 - e_b with e_b the largest
+  // biased exponent of the bounds fixc * rho^2 >= |block entry| of the items adding into block b,
+  // so |v * 2^se| < 2^50 (the 1.5 * 2^52 rounding constant below is exact there) and up to 2^13
+  // contributions never overflow. e_b is posted (ds_max_u32 into s_bx[k & 1][b], one per block of
+  // the item) at the end of chunk k-1 from its prefetched items. Per BLOCK (round 6; the chunk-wide
+  // exponent of rounds 4-5 summed a soft row beside stiff rows at the stiff rows' resolution, ~1e-13
+  // x the stiffness contrast): every cell adding into block (a, b) holds node a, so the block's
+  // scale is set by cells of its own row, and a row's error stays ~2^-50 of its own largest entry.
   auto bound_exp = [&](const Item& it, bool v) -> uint32_t {
     double rho = 0.0;
 #pragma unroll
@@ -2698,19 +2704,18 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
     const double m = P.fixc * rho * rho;
     return v ? (uint32_t)((uint64_t)__double_as_longlong(m) >> 52) & 0x7FFu : 0u;
   };
-  auto wave_max = [&](uint32_t e) -> uint32_t {
-    e = max(e, (uint32_t)__builtin_amdgcn_mov_dpp((int)e, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
-    e = max(e, (uint32_t)__builtin_amdgcn_mov_dpp((int)e, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
-    e = max(e, (uint32_t)__builtin_amdgcn_mov_dpp((int)e, 0x141, 0xF, 0xF, false));  // row_half_mirror
-    e = max(e, (uint32_t)__builtin_amdgcn_mov_dpp((int)e, 0x140, 0xF, 0xF, false));  // row_mirror
-    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)e, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)e, 16);
-    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)e, 32), dd = (uint32_t)__builtin_amdgcn_readlane((int)e, 48);
-    return max(max(a, b), max(c, dd));
+  auto post_bound = [&](const Item& it, const Desc& d, int par) {
+    if (jit < d.na) {
+      const uint32_t e = bound_exp(it, true);
+#pragma unroll
+      for (int bb = 0; bb < NBG; ++bb) {
+        const int s = (int)((it.sl[bb / 2] >> (16 * (bb % 2))) & 1023u);
+        if (s < d.nb) atomicMax(&s_bx[par * MAXB + s], e);
+      }
+    }
   };
-  auto post_bound = [&](const Item& it, const Desc& d, int slot) {
-    const uint32_t e = wave_max(bound_exp(it, jit < d.na));
-    if ((tid & 63) == 0) atomicMax(&s_fx[slot], e);
-  };
+  // 2^se of an exponent posted in s_bx (clamped: 2^(32 - se) stays finite)
+  auto blk_scale = [&](uint32_t e) -> int { return max(-990, min(990, 1072 - (int)e)); };
 
   Desc d0 = desc(0), d1 = desc(1), d2 = desc(2), d3 = desc(3);
   int32_t pf0 = load_entry(d0), pf1 = load_entry(d1), pf2 = FUSE ? load_entry(d2) : 0;
@@ -2751,12 +2756,6 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
     }
     const Desc d4 = desc(k + LOOK);
     if constexpr (!FIX) form_record(cur);  // FIX: formed at the end of the previous chunk (its bound)
-    int se = 0;
-    double S = 1.0;
-    if constexpr (FIX) {  // uniform: the scale's bits are built in SGPRs (2^se = (se + 1023) << 52)
-      se = __builtin_amdgcn_readfirstlane(max(-1000, min(1000, 1072 - (int)s_fx[k & 1])));
-      S = pow2(se);
-    }
     // items of chunk k
     const int64_t off = d0.b0 * BS2;
     const int h = (int)(off & 1);
@@ -2815,6 +2814,16 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
       };
       uint64_t qn = 0ull;
       if constexpr (!P1G) qn = Ah0[(cur.sl[0] >> 10) & 63u];
+      // FIX: the blocks' scale exponents, read together before the adds (one LDS wait, not one per block)
+      // (table blocks only: the fused P1 kernel has no registers to spare)
+      uint32_t ex[FIX ? NBG : 1];
+      if constexpr (FIX && !P1G) {
+#pragma unroll
+        for (int bb = 0; bb < NBG; ++bb) {
+          const int sb = (int)((cur.sl[bb / 2] >> (16 * (bb % 2))) & 1023u);
+          ex[bb] = s_bx[(k & 1) * MAXB + (eff ? sb : ((tid & 63) < nb ? (tid & 63) : 0))];
+        }
+      }
 #pragma unroll
       for (int bb = 0; bb < NBG; ++bb) {
         const uint32_t slv = (cur.sl[bb / 2] >> (16 * (bb % 2))) & 0xFFFFu;
@@ -2889,6 +2898,7 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
           const int sd = eff ? s : ((tid & 63) < nb ? (tid & 63) : 0);  // (zeros) distinct slots
           double* ap = acc + h + sd * BS2;
           if constexpr (FIX) {
+            const double S = pow2(blk_scale(P1G ? s_bx[(k & 1) * MAXB + sd] : ex[bb]));  // the block's scale
 #pragma unroll
             for (int i = 0; i < GD; ++i)
 #pragma unroll
@@ -2912,7 +2922,6 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
     // the exchanges at raised wave priority: they issue ahead of other workgroups' atomics on the
     // CU (E 37.4 -> 36.6 ms, C 1.15 -> 1.13 ms; over B1 .. B3: 36.7 / 1.12-1.13)
     __builtin_amdgcn_s_setprio(3);
-    if (FIX && tid == 0) s_fx[k & 1] = 0u;  // read by every item above; next written for chunk k + 2
     // read the chunk into registers and leave the accumulator zero: pairs t (value 2t + h .. 2t + 1 + h
     // at acc2[t + h]) by lane t % NT, the unpaired head (acc[1] when h = 1) by lane 0, the unpaired
     // tail by lane 1; no other lane touches them, so no barrier separates the reads from the zeroes
@@ -2938,16 +2947,20 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
       if (tid == 1 && tail) tv = xchg(acc + nv - 1 + h);
     }
     __builtin_amdgcn_s_setprio(0);
-    if constexpr (FIX) {  // the integer sums back to doubles: (hi 2^32 + lo) 2^-se, one rounding
-      const double c32 = pow2(32 - se), inv = pow2(-se);
-      auto tod = [&](double x) -> double {
+    if constexpr (FIX) {  // the integer sums back to doubles: (hi 2^32 + lo) 2^-se_b, one rounding
+      const uint32_t* bx = s_bx + (k & 1) * MAXB;
+      auto tod = [&](double x, int p) -> double {  // value p of the chunk (block p / BS2)
+        const int se = blk_scale(bx[min(max(p, 0) / BS2, MAXB - 1)]);
         const long long q = __double_as_longlong(x);
-        return fma((double)(int)(q >> 32), c32, (double)(unsigned)q * inv);
+        return fma((double)(int)(q >> 32), pow2(32 - se), (double)(unsigned)q * pow2(-se));
       };
 #pragma unroll
-      for (int u = 0; u < SW; ++u) v[u] = dv2{tod(v[u].x), tod(v[u].y)};
-      hv = tod(hv);
-      tv = tod(tv);
+      for (int u = 0; u < SW; ++u) {
+        const int p = 2 * (tid + NT * u) + h;  // pair t holds values 2t + h, 2t + h + 1
+        v[u] = dv2{tod(v[u].x, p), tod(v[u].y, p + 1)};
+      }
+      hv = tod(hv, 0);
+      tv = tod(tv, nv - 1);
     }
     // stores: SW pair stores + the head and the tail value on every lane (a static count: see above),
     // as buffer stores over the chunk's values; a lane without a pair (or the head / tail value)
@@ -2972,6 +2985,8 @@ __global__ __launch_bounds__(NT, NN == GD + 1 ? kLinWavesP1 : 4) void k_gather_l
     }
     __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics
     keep_vgprs(v, hv, tv);
+    if constexpr (FIX)  // chunk k's exponents are read; parity k & 1 is next posted at the end of chunk k + 1
+      for (int t = tid; t < nb; t += NT) s_bx[(k & 1) * MAXB + t] = 0u;
     // chunk k + AHEAD's id, read at iteration k + AHEAD - LOOK = k + 2 (after B1 of k + 1); written
     // here, where the wait for it is the one for chunk k+1's item loads (issued after it)
     if (tid == 0) s_id[(k + AHEAD) % RING] = chunk_of(rn);
@@ -3936,29 +3951,45 @@ extern "C" int fa_check_pattern(const fa_mesh* mesh, const fa_adjacency* adj, co
   return check_pattern(mesh, adj, indptr, indices, nblocks, true, stream);
 }
 
-__global__ void k_build_slots(MeshView M, const int64_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj_idx,
-                              const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
-                              uint16_t* __restrict__ slots, int* err) {
+// One wave per row (round 6; a thread per row took 0.21 s on config E): the row's columns are
+// staged in LDS (rows of up to kSlotCols blocks; longer rows search the pattern in memory) and the
+// lanes take the row's (adjacency entry, column node) pairs in order, so the slot writes of a row are
+// one contiguous run of u16.
+constexpr int kSlotCols = 1024;
+__global__ __launch_bounds__(64) void k_build_slots(MeshView M, const int64_t* __restrict__ adj_ptr,
+                                                    const int32_t* __restrict__ adj_idx,
+                                                    const int64_t* __restrict__ indptr,
+                                                    const int32_t* __restrict__ indices, uint16_t* __restrict__ slots,
+                                                    int* err) {
+  __shared__ int32_t cols[kSlotCols];
   const int nn = M.nn;
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < M.nnodes; r += (int64_t)gridDim.x * blockDim.x) {
+  const int lane = threadIdx.x;
+  for (int64_t r = blockIdx.x; r < M.nnodes; r += gridDim.x) {
     const int64_t b0 = indptr[r], b1 = indptr[r + 1];
-    if (b1 - b0 > 65535) {
-      atomicOr(err, 8);
+    const int64_t nb = b1 - b0;
+    if (nb > 65535) {
+      if (lane == 0) atomicOr(err, 8);
       continue;
     }
-    for (int64_t j = adj_ptr[r]; j < adj_ptr[r + 1]; ++j) {
-      const int64_t c = adj_idx[j] / nn;
-      for (int b = 0; b < nn; ++b) {
-        const int32_t col = M.cells[c * nn + b];
-        int64_t lo = b0, hi = b1 - 1, s = -1;
-        while (lo <= hi) {
-          int64_t mid = (lo + hi) >> 1;
-          if (indices[mid] == col) { s = mid; break; }
-          if (indices[mid] < col) lo = mid + 1; else hi = mid - 1;
-        }
-        if (s < 0) { atomicOr(err, 1); s = b0; }
-        slots[j * nn + b] = (uint16_t)(s - b0);
+    const bool inl = nb <= kSlotCols;
+    __syncthreads();  // the previous row's searches are done
+    if (inl)
+      for (int t = lane; t < nb; t += 64) cols[t] = indices[b0 + t];
+    __syncthreads();
+    const int64_t j0 = adj_ptr[r], nc = (adj_ptr[r + 1] - j0) * nn;
+    for (int64_t t = lane; t < nc; t += 64) {
+      const int64_t j = j0 + t / nn;
+      const int b = (int)(t % nn);
+      const int32_t col = M.cells[(int64_t)(adj_idx[j] / nn) * nn + b];
+      int64_t lo = 0, hi = nb - 1, s = -1;
+      while (lo <= hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const int32_t v = inl ? cols[mid] : indices[b0 + mid];
+        if (v == col) { s = mid; break; }
+        if (v < col) lo = mid + 1; else hi = mid - 1;
       }
+      if (s < 0) { atomicOr(err, 1); s = 0; }
+      slots[j * nn + b] = (uint16_t)s;
     }
   }
 }
@@ -3974,7 +4005,7 @@ extern "C" int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const
   HIP_TRY(hipMallocAsync((void**)&derr, sizeof(int), s));
   HIP_TRY(hipMemsetAsync(derr, 0, sizeof(int), s));
   if (mesh->nnodes > 0) {
-    k_build_slots<<<grid_for(mesh->nnodes), 256, 0, s>>>(M, adj->ptr, adj->idx, A->indptr, A->indices, slots, derr);
+    k_build_slots<<<grid_for(mesh->nnodes, 1), 64, 0, s>>>(M, adj->ptr, adj->idx, A->indptr, A->indices, slots, derr);
     LAUNCH_CHECK();
   }
   int herr = 0;
@@ -4285,7 +4316,9 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   // ordered entries pack (b << 10) | chunk-relative position (k_order_slots): keep the plain map
   // for a plan whose chunks could hold 1024 blocks or more
   if (plan->max_blocks >= 1024 || gather_maxb(false, mesh->gdim * mesh->gdim) >= 1024) return FA_OK;
-  const int groups = (kGatherMaxAdj * ns + 15) / 16;
+  // 16-lane quarters per chunk: the plan's largest chunk decides (round 6; every chunk had been given
+  // kGatherMaxAdj * ns / 16 threads, most of which found no items)
+  const int groups = (int)((std::min<int64_t>(std::max<int32_t>(plan->max_adj, 1), kGatherMaxAdj) * ns + 15) / 16);
   const int rounds = (plan->cell_flags & FA_PLAN_ORDER_SEARCH) ? kKempeRounds : 0;
   hipStream_t s = (hipStream_t)stream;
   const int64_t total = plan->nchunks * groups;
@@ -4374,12 +4407,26 @@ static int plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bs
   if (re0 <= rb0) { rb0 = 0; re0 = mesh->nnodes; }
   if (rb0 < 0 || re0 > mesh->nnodes) return fail(FA_E_ARG, "row window out of range");
   const int64_t n = re0;
-  std::vector<int64_t> ip(n + 1), ap(n + 1);
-  HIP_TRY(hipMemcpyAsync(ip.data(), A->indptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(ap.data(), adj->ptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, s));
+  // the two row pointer arrays and the chunk starts through pinned host memory (a pageable
+  // device-to-host copy of config E's 2 x 68 MB ran at a few hundred MB/s: most of the plan's host time)
+  int64_t* pin = nullptr;
+  const size_t pin_n = 2 * (size_t)(n + 1) + (size_t)(n - rb0) + 2;
+  HIP_TRY(hipHostMalloc((void**)&pin, sizeof(int64_t) * pin_n, hipHostMallocDefault));
+  struct PinFree { int64_t* p; ~PinFree() { (void)hipHostFree(p); } } pin_guard{pin};
+  int64_t* ip = pin;
+  int64_t* ap = pin + (n + 1);
+  int64_t* rsb = pin + 2 * (n + 1);
+  HIP_TRY(hipMemcpyAsync(ip, A->indptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(ap, adj->ptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  std::vector<int64_t> rs;
-  rs.reserve((n - rb0) / 8 + 2);
+  struct Starts {  // push_back into the pinned buffer (at most one start per row + the end)
+    int64_t* p;
+    size_t k;
+    void push_back(int64_t v) { p[k++] = v; }
+    int64_t back() const { return p[k - 1]; }
+    size_t size() const { return k; }
+    const int64_t* data() const { return p; }
+  } rs{rsb, 0};
   rs.push_back(rb0);
   int64_t start = rb0;
   int32_t mb = 0, ma = 0;

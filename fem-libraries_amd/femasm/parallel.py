@@ -372,6 +372,14 @@ class SlabProblem:
                                            if exchange == "oneway" else "a 2-rank all_reduce(SUM)")
                             + ", overlapping the interior rows")
 
+    def plan(self):
+        """Build the gather plans now (ghost mode plans lazily at the first assembly; the exchange
+        mode's SplitGather planned its row ranges at construction)."""
+        if self.mode == "ghost":
+            from . import fem
+
+            fem.gather_plan(self.V, self.A, 0, self.a.kind)
+
     def assemble(self, overlap: bool = True, check: bool = False):
         """Records of all cells; the interface-plane rows; their 2-rank all-reduces issued on
         RCCL's stream; the interior rows on the compute stream meanwhile; wait; bc diagonals.

@@ -68,14 +68,13 @@ extern "C" {
                                 then synchronise `stream` and return FA_E_PATTERN if a kernel found a (row,
                                 column) pair or a Dirichlet diagonal missing from the pattern (debugging) */
 /* Deterministic assembly (FA_DETERMINISTIC, or FA_PLAN_DETERMINISTIC in plan->cell_flags, which
- * fa_gather_rows honours too): the row gather adds every element contribution v of a row chunk as
- * the 64-bit integer round(v * 2^s) (s per chunk from a bound on its contributions, |v 2^s| < 2^50)
- * with integer LDS atomics, so each block's sum is exact and the same in any order, then converts
- * it back with one rounding: the values are identical run to run. Per value the result is within
- * ~2^-50 of the chunk's largest contribution bound per summand of the exact sum: a row of soft cells
- * that shares a chunk with much stiffer cells keeps ~1e-13 x (stiffness contrast) of its own scale
- * (6.8e-12 per row measured at a contrast of 100 inside chunks; the reference's E table spans 20, where
- * the 1e-12 bar holds; tests/test_gpu_deterministic.py). For affine-simplex
+ * fa_gather_rows honours too): the row gather adds every element contribution v to a block as the
+ * 64-bit integer round(v * 2^s_b) (s_b per BLOCK from a bound on the contributions of the cells adding
+ * into it, |v 2^s_b| < 2^50) with integer LDS atomics, so each block's sum is exact and the same in any
+ * order, then converts it back with one rounding: the values are identical run to run. Every cell
+ * adding into block (a, b) holds node a, so a row's values are within ~2^-50 per summand of its own
+ * cells' scale, at any stiffness contrast between rows (the per-row 1e-12 bar is tested at contrasts
+ * 1e2 .. 1e8, tests/test_gpu_deterministic.py; rounds 4-5 had one scale per row chunk). For affine-simplex
  * linear elasticity with one Poisson ratio (the k_gather_lin kernels) and a positional plan; other
  * forms return FA_E_UNSUPPORTED. (The reference's MFEM integrator is likewise order-fixed: it runs
  * one thread, MFEM/mechanic2d/asym_elasto_damage_model.cc:27.) */
