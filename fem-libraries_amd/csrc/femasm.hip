@@ -1410,7 +1410,9 @@ static constexpr int kGatherLdsValues = FA_GATHER_LDS;  // accumulator bytes per
 // neo-Hookean gather (2 workgroups / CU, VGPR-bound): a larger accumulator, and chunks capped at
 // 256 / NSPLIT adjacency entries so one chunk's items fill the workgroup's 256 lanes once
 // (fa_plan_gather_form); with the default plan ~96 entries -> 192 items left a wave idle
-constexpr int FA_GATHER_LDS_NEO = 46080;
+// (round 6: 41,472 = 576 blocks, so that the staged cell records (k_gather_neo<STG>) fit beside it at
+// 2 workgroups / CU; the neo plans' chunks are entry-bound at ~120 entries either way)
+constexpr int FA_GATHER_LDS_NEO = 41472;
 static constexpr int kGatherLdsNeo = FA_GATHER_LDS_NEO;
 constexpr int FA_NEO_NSPLIT = 2;  // neo-Hookean column items of 5 columns (E-neo at 2 waves / SIMD, round 2: NSPLIT 2
                                   // 342 ms, 5 at 3 waves 349, 10 at 4 waves 461; round 5: whole entries, 256
@@ -1513,6 +1515,11 @@ struct GatherArgs {
   const int64_t* cw;       // [nchunks + 1] offsets of the chunks' word sections (u16 units)
   const int32_t* ccells;   // [nchunks][FA_OWN_CCAP] the chunk's distinct cells (-1 padded)
   const uint16_t* cwords;  // per chunk: 256 lane starts, then K x 256 contribution words
+  // neo-Hookean chunk cell lists (fa_plan_cells) or NULL: each chunk's distinct cells at its first
+  // entries (ncell), each position's index in that list (nslot); k_gather_neo<STG> stages the
+  // chunk's cell records in LDS
+  const int32_t* ncell;
+  const uint8_t* nslot;
 };
 
 // The record of cell c for the gather (all kinds but the neo-Hookean tangents): see Rec.
@@ -3168,7 +3175,13 @@ __global__ __launch_bounds__(256, 3) void k_neo_records_m(MeshView M, FormView F
 }
 
 // 2 waves / SIMD (215 VGPRs, no spills in the item loop; 3 waves measured slower: spilled records)
-template <int GD, int NN, int NQ, int NSPLIT>
+// STG (round 6, plans with fa_plan_cells' lists): the records of a chunk's distinct cells are staged in
+// LDS by the whole workgroup with coalesced 16-B loads -- each cell's record once, as ~24 lanes of one
+// wave instruction -- one chunk ahead (issued after the items, written after the drain), and every
+// item reads its cell's record from LDS. Without STG every item loads its own cell's 376-B record with
+// scattered 16-B loads (two items per entry, ~1.6 entries per cell per chunk: each record fetched ~3
+// times, 24 load instructions of ~32 cache lines each per lane).
+template <int GD, int NN, int NQ, int NSPLIT, bool STG = false>
 __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint32_t* __restrict__ zero32,
                                                        double* __restrict__ dump, int64_t per) {
   using R = NeoM<GD, NQ>;
@@ -3187,6 +3200,12 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
   __shared__ __attribute__((aligned(16))) double acc[2 * NP2];
   __shared__ __attribute__((aligned(16))) double s_phi[NN * NQ * GD];  // [b][q][k]: a column's gradients at every point, contiguous
   __shared__ __attribute__((aligned(16))) double s_T[NN * NN * NT];    // [a][b][t]
+  // STG: the chunk's cell records ([slot][head | points], padded to RSTR doubles: 4 banks apart) and
+  // the cell lists of the chunks of both parities ahead (-1 past a chunk's last cell)
+  constexpr int CCAP = FA_NEO_CELL_CAP, NPC = R::SIZE / 2, RSTR = R::SIZE + 2;
+  constexpr int NRS = (CCAP * NPC + 255) / 256;  // staged 16-B pieces per lane
+  __shared__ __attribute__((aligned(16))) double s_rec[STG ? CCAP * RSTR : 2];
+  __shared__ int32_t s_cl[STG ? 2 * CCAP : 1];
   dv2* acc2 = reinterpret_cast<dv2*>(acc);
   const int tid = threadIdx.x;
   // chunk schedule of k_gather_lin (round 5): the resident grid pulls chunks from 8 per-XCD counters,
@@ -3252,9 +3271,15 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
   auto load_entry = [&](const Desc& d) -> int32_t { return eadj[entry_of(d)]; };
   // the head's S and s_c (NT + 1 values; its padding is not loaded); slots two per register
   constexpr int HL = NT + 1, NSL = (NBG + 1) / 2;
-  struct Item { double hd[HL]; double pt[NQL][R::PT]; uint32_t sl[NSL]; uint32_t mask; };
+  struct Item { double hd[HL]; double pt[NQL][R::PT]; uint32_t sl[NSL]; uint32_t mask; uint32_t cs; };
   auto load_item = [&](const Desc& d, int32_t pflat, Item& it) {
     const int64_t c = pflat / NN;
+    if constexpr (STG) {  // the record comes from the staged cells (stage_* below): its slot only
+      load_slot_words<NN, NSPLIT>(P.slots, entry_of(d), part, it.sl);
+      it.mask = mk[c * mkmul] * mkmul;
+      it.cs = P.nslot[entry_of(d)];
+      return;
+    }
     const double* hq = P.rec + R::head(c);
     const dv2* hp = reinterpret_cast<const dv2*>(hq);
 #pragma unroll
@@ -3277,11 +3302,72 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
     load_slot_words<NN, NSPLIT>(P.slots, entry_of(d), part, it.sl);
     it.mask = mk[c * mkmul] * mkmul;
   };
+  // STG: a chunk's cell list (lane t < CCAP: its t-th cell, -1 past the last) and its records, piece
+  // f = tid + 256 r of the staging = cell f / NPC, 16-B piece f % NPC of [head | points]
+  auto list_load = [&](const Desc& d) -> int32_t {
+    return (tid < CCAP && tid < d.na) ? P.ncell[d.a0 + tid] : -1;
+  };
+  // (the lane's piece indices are recomputed at every use from an opaque copy of tid: hoisted out of the
+  // chunk loop they were 16 registers live through the items, and spilled)
+  auto stage_load = [&](int par, dv2 (&g)[NRS]) {
+    int t0 = tid;
+    asm volatile("" : "+v"(t0));
+#pragma unroll
+    for (int r = 0; r < NRS; ++r) {
+      const int f = t0 + 256 * r, i = min(f / NPC, CCAP - 1), j = f % NPC;
+      int32_t c = s_cl[par * CCAP + i];
+      c = c >= 0 ? c : max(s_cl[par * CCAP], 0);  // (past the list: any valid record; not written)
+      // NeoM tiles: [64 heads][point 0: 64 x PT] ..., cell c at tile c >> 6, lane c & 63
+      const bool hd = j < R::HEAD / 2;
+      const int jq = (j - R::HEAD / 2) / (R::PT / 2), jk = (j - R::HEAD / 2) % (R::PT / 2);
+      const int in_tile = hd ? (c & 63) * R::HEAD + 2 * j : 64 * R::HEAD + jq * (64 * R::PT) + (c & 63) * R::PT + 2 * jk;
+      g[r] = *reinterpret_cast<const dv2*>(P.rec + (int64_t)(c >> 6) * (64 * R::SIZE) + in_tile);
+    }
+  };
+  auto stage_store = [&](int par, const dv2 (&g)[NRS]) {
+    int t0 = tid;
+    asm volatile("" : "+v"(t0));
+#pragma unroll
+    for (int r = 0; r < NRS; ++r) {
+      const int f = t0 + 256 * r, i = f / NPC, j = f % NPC;
+      if (i < CCAP && s_cl[par * CCAP + i] >= 0) *reinterpret_cast<dv2*>(s_rec + i * RSTR + 2 * j) = g[r];
+    }
+  };
+  // STG: the item's record from its cell's staged copy
+  auto read_rec = [&](Item& it) {
+    const double* rp = s_rec + min((int)it.cs, CCAP - 1) * RSTR;
+#pragma unroll
+    for (int k = 0; k < HL / 2; ++k) {
+      const dv2 v = *reinterpret_cast<const dv2*>(rp + 2 * k);
+      it.hd[2 * k] = v.x;
+      it.hd[2 * k + 1] = v.y;
+    }
+    if constexpr (HL % 2) it.hd[HL - 1] = rp[HL - 1];
+#pragma unroll
+    for (int ql = 0; ql < NQL; ++ql)
+#pragma unroll
+      for (int k = 0; k < R::PT / 2; ++k) {
+        const dv2 v = *reinterpret_cast<const dv2*>(rp + R::HEAD + ql * R::PT + 2 * k);
+        it.pt[ql][2 * k] = v.x;
+        it.pt[ql][2 * k + 1] = v.y;
+      }
+  };
 
   Desc d0 = desc(0), d1 = desc(1), d2 = desc(2);
   int32_t pf0 = load_entry(d0), pf1 = load_entry(d1);
   Item cur;
   load_item(d0, pf0, cur);
+  if constexpr (STG) {  // chunk 0's records and chunk 1's list staged before the loop
+    if (tid < CCAP) {
+      s_cl[tid] = list_load(d0);
+      s_cl[CCAP + tid] = list_load(d1);
+    }
+    __syncthreads();
+    dv2 g[NRS];
+    stage_load(0, g);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    stage_store(0, g);
+  }
   int bad = 0;
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the prologue's loads (see k_gather_lin)
   __syncthreads();                     // tables and accumulator staged
@@ -3294,6 +3380,7 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
     const int h = (int)(off & 1);
     const int nb = d0.nb;
     const bool valid = jit < d0.na;
+    if constexpr (STG) read_rec(cur);
     {
       const int aloc = pf0 % NN;
       const uint32_t rowm = (cur.mask >> (aloc * GD)) & ((1u << GD) - 1);
@@ -3400,10 +3487,22 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
     // chunk k+1's records / slots / masks: the item registers are dead here, and these loads are
     // issued before chunk k's stores (their wait at chunk k+1 does not include the stores)
     load_item(d1, pf1, cur);
+    // STG: chunk k+1's staged records and chunk k+2's cell list, loaded now, written to LDS after the
+    // drain (the items of chunk k have read s_rec by B1)
+    dv2 g[STG ? NRS : 1];
+    int32_t cl2 = -1;
+    if constexpr (STG) {
+      stage_load((k + 1) & 1, g);
+      cl2 = list_load(d2);
+    }
     __syncthreads();  // B1: the chunk is accumulated
     fa_dv2 dv[SW];
     double dh, dt;
     xchg_drain<SW, NTH>(acc, h, nb * BS2, P.A.data + off, tid, dv, dh, dt);
+    if constexpr (STG) {
+      stage_store((k + 1) & 1, g);
+      if (tid < CCAP) s_cl[(k & 1) * CCAP + tid] = cl2;  // parity of k + 2
+    }
     __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics
     keep_vgprs(dv, dh, dt);
     // chunk k + AHEAD's id, read at iteration k + AHEAD - LOOK (after later barriers)
@@ -4017,6 +4116,8 @@ extern "C" int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const
   plan->slots = slots;
   plan->slot_order = 0;
   plan->eadj = nullptr;
+  plan->ccell = nullptr;
+  plan->cslot = nullptr;
   return FA_OK;
 }
 
@@ -4219,13 +4320,23 @@ __global__ __launch_bounds__(kOrderThreads) void k_order_slots(const int64_t* __
 // collects many more adds than the quarter has steps; the order search then spreads them over
 // the steps. Writes eperm (position -> entry offset) and eadj (the entries' adjacency values in
 // position order). One thread per chunk.
-template <int NN, int NSPLIT>
-__global__ void k_plan_perm(const int64_t* __restrict__ row_start, const int64_t* __restrict__ indptr,
-                            const int64_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj_idx,
-                            int64_t nchunks, const uint16_t* __restrict__ src, uint16_t* __restrict__ eperm,
-                            int32_t* __restrict__ eadj) {
+// The residue histograms and fill counts of a chunk's quarters live in LDS (round 6: a thread's 1 KB
+// array of up to 64 quarters sat in scratch; config E's plan step 0.10 s), sized by MQ quarters: the
+// host picks MQ = 16 when every chunk holds at most 16 quarters (the k_gather_lin / k_gather_neo
+// plans: <= 256 items per chunk), else kGatherMaxAdj / EQ.
+constexpr int kPermThreads = 64;
+template <int NN, int NSPLIT, int MQ>
+__global__ __launch_bounds__(kPermThreads) void k_plan_perm(const int64_t* __restrict__ row_start,
+                                                            const int64_t* __restrict__ indptr,
+                                                            const int64_t* __restrict__ adj_ptr,
+                                                            const int32_t* __restrict__ adj_idx, int64_t nchunks,
+                                                            const uint16_t* __restrict__ src,
+                                                            uint16_t* __restrict__ eperm, int32_t* __restrict__ eadj) {
   constexpr int EQ = NSPLIT <= 16 ? 16 / NSPLIT : 1;  // entries per quarter (host: only for 16 % NSPLIT == 0)
-  constexpr int MQ = kGatherMaxAdj / EQ;       // quarters per chunk, at most
+  constexpr int TH = MQ <= 16 ? kPermThreads : 16;  // threads per workgroup (the host launches TH)
+  __shared__ uint8_t s_h[TH][MQ][16], s_fill[TH][MQ];
+  auto& h = s_h[threadIdx.x];
+  auto& fill = s_fill[threadIdx.x];
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nchunks;
        c += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r0 = row_start[c], r1 = row_start[c + 1];
@@ -4233,8 +4344,7 @@ __global__ void k_plan_perm(const int64_t* __restrict__ row_start, const int64_t
     const int na = (int)(adj_ptr[r1] - a0);
     if (na <= 0) continue;
     const int64_t b0 = indptr[r0];
-    const int nq = (na + EQ - 1) / EQ;
-    uint8_t h[MQ][16], fill[MQ];
+    const int nq = min((na + EQ - 1) / EQ, MQ);
     for (int q = 0; q < nq; ++q) {
       fill[q] = 0;
       for (int r = 0; r < 16; ++r) h[q][r] = 0;
@@ -4267,6 +4377,94 @@ __global__ void k_plan_perm(const int64_t* __restrict__ row_start, const int64_t
       eadj[a0 + pos] = adj_idx[e];
     }
   }
+}
+
+// fa_plan_cells: one wave per chunk: the chunk's positional entries' cells (eadj / NN) bitonic-sorted in
+// LDS, the distinct ones listed at ccell[a0 ..), -1 after; every position's index in that list by
+// binary search. Chunks with more than FA_NEO_CELL_CAP cells set *over.
+template <int NN>
+__global__ __launch_bounds__(64) void k_plan_cells(const int64_t* __restrict__ row_start,
+                                                   const int64_t* __restrict__ adj_ptr, const int32_t* __restrict__ eadj,
+                                                   int64_t nchunks, int32_t* __restrict__ ccell,
+                                                   uint8_t* __restrict__ cslot, int* over) {
+  __shared__ int32_t s[kGatherMaxAdj], u[kGatherMaxAdj];
+  const int lane = threadIdx.x;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t a0 = adj_ptr[row_start[c]];
+    const int na = (int)min<int64_t>(adj_ptr[row_start[c + 1]] - a0, kGatherMaxAdj);
+    int n2 = 1;
+    while (n2 < na) n2 <<= 1;
+    __syncthreads();
+    for (int t = lane; t < n2; t += 64) s[t] = t < na ? eadj[a0 + t] / NN : INT32_MAX;
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int t = lane; t < n2; t += 64) {
+          const int x = t ^ j;
+          if (x > t) {
+            const int32_t a = s[t], b = s[x];
+            if ((a > b) == ((t & k) == 0)) { s[t] = b; s[x] = a; }
+          }
+        }
+        __syncthreads();
+      }
+    int nu = 0;
+    for (int t0 = 0; t0 < n2; t0 += 64) {
+      const int t = t0 + lane;
+      const int32_t v = t < n2 ? s[t] : INT32_MAX;
+      const bool keep = v != INT32_MAX && (t == 0 || s[t - 1] != v);
+      const unsigned long long m = __ballot(keep);
+      if (keep) u[nu + __popcll(m & ((1ull << lane) - 1ull))] = v;
+      nu += __popcll(m);
+    }
+    __syncthreads();
+    for (int t = lane; t < na; t += 64) ccell[a0 + t] = t < nu ? u[t] : -1;
+    for (int t = lane; t < na; t += 64) {
+      const int32_t v = eadj[a0 + t] / NN;
+      int lo = 0, hi = nu - 1, f = 0;
+      while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        if (u[mid] == v) { f = mid; break; }
+        if (u[mid] < v) lo = mid + 1; else hi = mid - 1;
+      }
+      cslot[a0 + t] = (uint8_t)min(f, 255);
+    }
+    if (lane == 0 && nu > FA_NEO_CELL_CAP) atomicOr(over, 1);
+  }
+}
+
+extern "C" int fa_plan_cells(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int32_t* ccell,
+                             uint8_t* cslot, fa_plan* plan, void* stream) {
+  int rc = check_mesh(mesh);
+  if (rc) return rc;
+  if (!adj || !A || !ccell || !cslot || !plan) return fail(FA_E_ARG, "null argument");
+  plan->ccell = nullptr;
+  plan->cslot = nullptr;
+  if (!plan->eadj || !plan->row_start || plan->nchunks <= 0) return FA_OK;  // no positional plan: nothing to list
+  if (!(plan->cell_flags & FA_PLAN_NEO)) return FA_OK;  // only the neo-Hookean gather stages cell records
+  hipStream_t s = (hipStream_t)stream;
+  int* over = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&over, sizeof(int), s));
+  HIP_TRY(hipMemsetAsync(over, 0, sizeof(int), s));
+  const int grid = (int)std::min<int64_t>(plan->nchunks, kMaxBlocks);
+  bool ok = true;
+  switch (mesh->nn) {
+    case 10: k_plan_cells<10><<<grid, 64, 0, s>>>(plan->row_start, adj->ptr, plan->eadj, plan->nchunks, ccell, cslot, over); break;
+    case 6: k_plan_cells<6><<<grid, 64, 0, s>>>(plan->row_start, adj->ptr, plan->eadj, plan->nchunks, ccell, cslot, over); break;
+    default: ok = false;
+  }
+  int ho = 1;
+  if (ok) {
+    LAUNCH_CHECK();
+    HIP_TRY(hipMemcpyAsync(&ho, over, sizeof(int), hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(hipFreeAsync(over, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (ok && !ho) {
+    plan->ccell = ccell;
+    plan->cslot = cslot;
+  }
+  return FA_OK;
 }
 
 // NSPLIT of the affine-simplex linear-elasticity gather kernel for (cell, degree, quadrature
@@ -4307,6 +4505,8 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   if (!plan->slots) return fail(FA_E_ARG, "fa_plan_order needs the slot map (fa_plan_slots first)");
   plan->slot_order = 0;
   plan->eadj = nullptr;
+  plan->ccell = nullptr;  // cell lists are of a positional order: fa_plan_cells after this
+  plan->cslot = nullptr;
   DevTables T;
   if ((rc = get_tables(mesh->cell_type, mesh->degree, -1, &T))) return rc;
   const int ns = (plan->cell_flags & FA_PLAN_NEO) && is_simplex(mesh->cell_type)
@@ -4330,6 +4530,8 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   const bool posn = eadj != nullptr && 16 % ns == 0 && !(tensor && mesh->nn * mesh->gdim > 32);
   uint16_t *src = nullptr, *eperm = nullptr;
   const int64_t nent = mesh->ncells * mesh->nn;
+  // k_plan_perm's quarter arrays: 16 quarters cover every chunk of <= 16 x 16 items
+  const bool small_q = (int64_t)std::max<int32_t>(plan->max_adj, 1) * ns <= 256;
   if (posn) {
     HIP_TRY(hipMallocAsync((void**)&src, sizeof(uint16_t) * nent * mesh->nn, s));
     HIP_TRY(hipMallocAsync((void**)&eperm, sizeof(uint16_t) * nent, s));
@@ -4337,9 +4539,12 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   }
 #define ORD(NN_, NS_)                                                                                         \
   do {                                                                                                        \
-    if (posn)                                                                                                 \
-      k_plan_perm<NN_, NS_><<<grid_for(plan->nchunks), 64, 0, s>>>(plan->row_start, A->indptr, adj->ptr,      \
-                                                                   adj->idx, plan->nchunks, src, eperm, eadj);   \
+    if (posn && small_q)                                                                                      \
+      k_plan_perm<NN_, NS_, 16><<<grid_for(plan->nchunks, kPermThreads), kPermThreads, 0, s>>>(               \
+          plan->row_start, A->indptr, adj->ptr, adj->idx, plan->nchunks, src, eperm, eadj);                      \
+    else if (posn)                                                                                            \
+      k_plan_perm<NN_, NS_, kGatherMaxAdj / (NS_ <= 16 ? 16 / NS_ : 1)><<<grid_for(plan->nchunks, 16), 16, 0, s>>>( \
+          plan->row_start, A->indptr, adj->ptr, adj->idx, plan->nchunks, src, eperm, eadj);                      \
     k_order_slots<NN_, NS_><<<grid_for(total, kOrderThreads), kOrderThreads, 0, s>>>(plan->row_start, A->indptr, adj->ptr, plan->nchunks, \
                                                             groups, sl, src, eperm, rounds);                   \
   } while (0)
@@ -4396,6 +4601,55 @@ __global__ void k_check_affine(MeshView M, int* nonaffine) {
   }
 }
 
+// plan_gather's device chunking: segment t = rows [rb0 + t * kChunkSeg, ...) cut greedily by one thread
+// (a new chunk when the next row would exceed maxb blocks, maxadj entries or kGatherMaxRows rows; a row
+// over a cap is reported), its starts at tmp[t * kChunkSeg + k], its count in cnt[t]
+constexpr int64_t kChunkSeg = 2048;
+__global__ void k_chunk_seg(const int64_t* __restrict__ ip, const int64_t* __restrict__ ap, int64_t rb0, int64_t n,
+                            int64_t maxb, int maxadj, int64_t* __restrict__ tmp, int64_t* __restrict__ cnt,
+                            int* __restrict__ st) {
+  const int64_t nseg = (n - rb0 + kChunkSeg - 1) / kChunkSeg;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nseg; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r0 = rb0 + t * kChunkSeg, r1 = min(n, r0 + kChunkSeg);
+    int64_t* out = tmp + t * kChunkSeg;
+    int64_t k = 0, start = r0;
+    int mb = 0, ma = 0, bad = INT32_MAX;
+    int64_t ipr = ip[r0], apr = ap[r0], ips = ipr, aps = apr;
+    out[k++] = r0;
+    for (int64_t r = r0; r < r1; ++r) {
+      const int64_t ipn = ip[r + 1], apn = ap[r + 1];
+      if ((ipn - ipr > maxb || apn - apr > kGatherMaxAdj) && bad == INT32_MAX) bad = (int)(r - rb0);
+      // maxadj is a target: a row with more entries gets a chunk of its own
+      if (r > start && (ipn - ips > maxb || apn - aps > maxadj || r + 1 - start > kGatherMaxRows)) {
+        out[k++] = r;
+        mb = max(mb, (int)(ipr - ips));
+        ma = max(ma, (int)(apr - aps));
+        start = r;
+        ips = ipr;
+        aps = apr;
+      }
+      ipr = ipn;
+      apr = apn;
+    }
+    mb = max(mb, (int)(ipr - ips));
+    ma = max(ma, (int)(apr - aps));
+    cnt[t] = k;
+    atomicMax(&st[0], mb);
+    atomicMax(&st[1], ma);
+    if (bad != INT32_MAX) atomicMin(&st[2], bad);
+  }
+}
+// row_start[off[t] + k] = tmp[t * kChunkSeg + k] for k < count of segment t; row_start[total] = n
+__global__ void k_chunk_compact(const int64_t* __restrict__ tmp, const int64_t* __restrict__ off, int64_t rb0, int64_t n,
+                                int64_t* __restrict__ row_start) {
+  const int64_t nrows = n - rb0, nseg = (nrows + kChunkSeg - 1) / kChunkSeg;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = i / kChunkSeg, k = i % kChunkSeg;
+    if (off[t] + k < off[t + 1]) row_start[off[t] + k] = tmp[i];
+    if (i == 0) row_start[off[nseg]] = n;
+  }
+}
+
 // chunk rows so each chunk's blocks fit `maxb` accumulator blocks and its adjacency `maxadj`
 static int plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int64_t* row_start,
                        fa_plan* plan, void* stream, int64_t maxb, int maxadj) {
@@ -4407,50 +4661,56 @@ static int plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bs
   if (re0 <= rb0) { rb0 = 0; re0 = mesh->nnodes; }
   if (rb0 < 0 || re0 > mesh->nnodes) return fail(FA_E_ARG, "row window out of range");
   const int64_t n = re0;
-  // the two row pointer arrays and the chunk starts through pinned host memory (a pageable
-  // device-to-host copy of config E's 2 x 68 MB ran at a few hundred MB/s: most of the plan's host time)
-  int64_t* pin = nullptr;
-  const size_t pin_n = 2 * (size_t)(n + 1) + (size_t)(n - rb0) + 2;
-  HIP_TRY(hipHostMalloc((void**)&pin, sizeof(int64_t) * pin_n, hipHostMallocDefault));
-  struct PinFree { int64_t* p; ~PinFree() { (void)hipHostFree(p); } } pin_guard{pin};
-  int64_t* ip = pin;
-  int64_t* ap = pin + (n + 1);
-  int64_t* rsb = pin + 2 * (n + 1);
-  HIP_TRY(hipMemcpyAsync(ip, A->indptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(ap, adj->ptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  struct Starts {  // push_back into the pinned buffer (at most one start per row + the end)
-    int64_t* p;
-    size_t k;
-    void push_back(int64_t v) { p[k++] = v; }
-    int64_t back() const { return p[k - 1]; }
-    size_t size() const { return k; }
-    const int64_t* data() const { return p; }
-  } rs{rsb, 0};
-  rs.push_back(rb0);
-  int64_t start = rb0;
-  int32_t mb = 0, ma = 0;
-  for (int64_t r = rb0; r < n; ++r) {
-    int64_t rb = ip[r + 1] - ip[r], ra = ap[r + 1] - ap[r];
-    if (rb > maxb || ra > kGatherMaxAdj)
-      return fail(FA_E_CAPACITY, "row %lld has %lld blocks / %lld cells (gather caps %lld / %d): use FA_SCATTER",
-                  (long long)r, (long long)rb, (long long)ra, (long long)maxb, kGatherMaxAdj);
-    // maxadj is a target: a row with more entries gets a chunk of its own
-    int64_t cb = ip[r + 1] - ip[start], ca = ap[r + 1] - ap[start];
-    if (r > start && (cb > maxb || ca > maxadj || r + 1 - start > kGatherMaxRows)) {
-      rs.push_back(r);
-      mb = std::max<int32_t>(mb, (int32_t)(ip[r] - ip[start]));
-      ma = std::max<int32_t>(ma, (int32_t)(ap[r] - ap[start]));
-      start = r;
-    }
+  // Greedy chunking on the device (round 6; the host loop over config E's 67 M rows with their two
+  // row pointer arrays copied to the host took 0.3-0.4 s of the plan): the window is cut into
+  // segments of kChunkSeg rows, one thread each runs the greedy cut over its segment (a chunk always
+  // starts at a segment's first row: one extra cut per kChunkSeg rows), then the per-segment starts
+  // are compacted behind an exclusive scan of their counts.
+  const int64_t nrows = n - rb0;
+  const int64_t nseg = (nrows + kChunkSeg - 1) / kChunkSeg;  // 0 for an empty window
+  int64_t* tmp = nullptr;   // [nrows] per-segment chunk starts (segment t at t * kChunkSeg)
+  int64_t* cnt = nullptr;   // [nseg + 1] counts, then offsets
+  int* st = nullptr;        // [4]: max blocks, max entries, first row over a cap (INT_MAX: none)
+  void* scan_tmp = nullptr;
+  size_t scan_bytes = 0;
+  if ((rc = scratch_alloc((void**)&tmp, sizeof(int64_t) * (size_t)std::max<int64_t>(nrows, 1), s))) return rc;
+  if ((rc = scratch_alloc((void**)&cnt, sizeof(int64_t) * (size_t)(nseg + 1), s))) return rc;
+  if ((rc = scratch_alloc((void**)&st, sizeof(int) * 4, s))) return rc;
+  static const int st0[4] = {0, 0, INT32_MAX, 0};
+  HIP_TRY(hipMemcpyAsync(st, st0, sizeof(st0), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(int64_t) * (size_t)(nseg + 1), s));
+  if (nseg > 0) {
+    k_chunk_seg<<<grid_for(nseg, 64), 64, 0, s>>>(A->indptr, adj->ptr, rb0, n, maxb, maxadj, tmp, cnt, st);
+    LAUNCH_CHECK();
   }
-  if (rs.back() != n) {
-    mb = std::max<int32_t>(mb, (int32_t)(ip[n] - ip[start]));
-    ma = std::max<int32_t>(ma, (int32_t)(ap[n] - ap[start]));
-    rs.push_back(n);
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, cnt, cnt, (int)(nseg + 1), s));
+  if ((rc = scratch_alloc(&scan_tmp, std::max<size_t>(scan_bytes, 16), s))) return rc;
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, cnt, cnt, (int)(nseg + 1), s));
+  if (nrows > 0) {
+    k_chunk_compact<<<grid_for(nrows), 256, 0, s>>>(tmp, cnt, rb0, n, row_start);
+    LAUNCH_CHECK();
+  } else {
+    HIP_TRY(hipMemcpyAsync(row_start, &rb0, sizeof(int64_t), hipMemcpyHostToDevice, s));
   }
-  HIP_TRY(hipMemcpyAsync(row_start, rs.data(), sizeof(int64_t) * rs.size(), hipMemcpyHostToDevice, s));
+  int64_t total = 0;
+  int sth[3] = {0, 0, 0};
+  HIP_TRY(hipMemcpyAsync(&total, cnt + nseg, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(sth, st, sizeof(int) * 3, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipFreeAsync(scan_tmp, s));
+  HIP_TRY(hipFreeAsync(tmp, s));
+  HIP_TRY(hipFreeAsync(cnt, s));
+  HIP_TRY(hipFreeAsync(st, s));
   HIP_TRY(hipStreamSynchronize(s));
+  if (sth[2] != INT32_MAX && sth[2] >= 0) {
+    int64_t r = rb0 + sth[2], rp[2][2];
+    HIP_TRY(hipMemcpy(rp[0], A->indptr + r, sizeof(int64_t) * 2, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(rp[1], adj->ptr + r, sizeof(int64_t) * 2, hipMemcpyDeviceToHost));
+    return fail(FA_E_CAPACITY, "row %lld has %lld blocks / %lld cells (gather caps %lld / %d): use FA_SCATTER",
+                (long long)r, (long long)(rp[0][1] - rp[0][0]), (long long)(rp[1][1] - rp[1][0]), (long long)maxb,
+                kGatherMaxAdj);
+  }
+  const int32_t mb = sth[0], ma = sth[1];
+  struct { int64_t k; int64_t size() const { return k; } } rs{total + 1};
   plan->nchunks = (int64_t)rs.size() - 1;
   plan->row_start = row_start;
   plan->cell_flags = 0;
@@ -4475,6 +4735,8 @@ static int plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bs
   plan->eadj = nullptr;
   plan->corder = nullptr;
   plan->contrib = nullptr;
+  plan->ccell = nullptr;
+  plan->cslot = nullptr;
   return FA_OK;
 }
 
@@ -4716,6 +4978,8 @@ extern "C" int fa_plan_contrib(const fa_mesh* mesh, const fa_adjacency* adj, con
 
 // the kernel's views of plan->contrib (NULL pointers without one)
 static void set_contrib(GatherArgs& P, const fa_plan* plan) {
+  P.ncell = plan ? plan->ccell : nullptr;
+  P.nslot = plan && plan->ccell ? plan->cslot : nullptr;
   P.cw = nullptr;
   P.ccells = nullptr;
   P.cwords = nullptr;
@@ -5093,8 +5357,13 @@ static int launch_gather_neo(GatherArgs P, const int8_t* bc, hipStream_t s, cons
     if ((rc = lin_scratch(&zero32, &dump))) return rc;
     int64_t* ldesc = nullptr;
     if ((rc = lin_chunk_desc(P, &ldesc, s, P.corder))) return rc;
-    const int64_t grid = gather_grid(k_gather_neo<GD, NN, NQ, NSPLIT>, P.nchunks, 256);
-    k_gather_neo<GD, NN, NQ, NSPLIT><<<(unsigned)grid, 256, 0, s>>>(P, zero32, dump, (P.nchunks + 7) / 8);
+    if (P.ncell && P.nslot) {  // chunk cell lists (fa_plan_cells): records staged per chunk in LDS
+      const int64_t grid = gather_grid(k_gather_neo<GD, NN, NQ, NSPLIT, true>, P.nchunks, 256);
+      k_gather_neo<GD, NN, NQ, NSPLIT, true><<<(unsigned)grid, 256, 0, s>>>(P, zero32, dump, (P.nchunks + 7) / 8);
+    } else {
+      const int64_t grid = gather_grid(k_gather_neo<GD, NN, NQ, NSPLIT>, P.nchunks, 256);
+      k_gather_neo<GD, NN, NQ, NSPLIT><<<(unsigned)grid, 256, 0, s>>>(P, zero32, dump, (P.nchunks + 7) / 8);
+    }
     LAUNCH_CHECK();
     HIP_TRY(hipFreeAsync(ldesc, s));
     if (bc) {  // Dirichlet diagonals (dolfinx set_diagonal) of the plan's rows

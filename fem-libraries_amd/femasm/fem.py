@@ -538,11 +538,9 @@ def check_pattern(V: FunctionSpace, indptr: torch.Tensor, indices: torch.Tensor)
                "fa_check_pattern")
 
 
-def create_matrix(a, max_part_bytes: int | None = None, check: bool = False) -> MatrixCSR:
-    """Sparsity pattern of the bilinear form (all node pairs of every cell), built on the GPU
-    (dolfinx.fem.petsc.create_matrix, FEniCSx/mechanic2d/asym_elasto_damage_model.cc:688).
-    check: validate the pattern and adjacency on the device (fa_check_pattern)."""
-    V = a.V
+def sparsity_pattern(V: FunctionSpace):
+    """The BSR pattern (indptr, indices) of V's cell node pairs, built on the GPU once and cached on V
+    (dolfinx.fem.create_sparsity_pattern; create_matrix uses it)."""
     if V._pattern is None:
         L = _lib.load()
         dev = V.mesh.device
@@ -557,7 +555,15 @@ def create_matrix(a, max_part_bytes: int | None = None, check: bool = False) -> 
         _lib.check(L.fa_sparsity_fill(ctypes.byref(fm), ctypes.byref(adj), indptr.data_ptr(), indices.data_ptr(), sh),
                    "fa_sparsity_fill")
         V._pattern = (indptr, indices)
-    indptr, indices = V._pattern
+    return V._pattern
+
+
+def create_matrix(a, max_part_bytes: int | None = None, check: bool = False) -> MatrixCSR:
+    """Sparsity pattern of the bilinear form (all node pairs of every cell), built on the GPU
+    (dolfinx.fem.petsc.create_matrix, FEniCSx/mechanic2d/asym_elasto_damage_model.cc:688), and the
+    matrix's value array. check: validate the pattern and adjacency on the device (fa_check_pattern)."""
+    V = a.V
+    indptr, indices = sparsity_pattern(V)
     if check:
         check_pattern(V, indptr, indices)
     if max_part_bytes is None:
@@ -603,6 +609,19 @@ def _plan_locality(V, fm, adj, plan, sh, locality: bool = True):
     return corder if plan.corder else None
 
 
+def _plan_cells(V, fm, adj, fb, plan, sh):
+    """Each chunk's distinct cells and every position's index among them (fa_plan_cells): the neo-Hookean
+    gather then stages the chunk's cell records in LDS with coalesced loads. Returns the buffers (kept
+    with the plan), or None when a chunk has more cells than the kernel's staging holds (the gather then
+    loads every item's record itself)."""
+    nent = V.mesh.num_cells * V.nn
+    ccell = torch.empty(max(nent, 1), dtype=torch.int32, device=V.mesh.device)
+    cslot = torch.empty(max(nent, 1), dtype=torch.uint8, device=V.mesh.device)
+    _lib.check(_lib.load().fa_plan_cells(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), ccell.data_ptr(),
+                                         cslot.data_ptr(), ctypes.byref(plan), sh), "fa_plan_cells")
+    return (ccell, cslot) if plan.ccell else None
+
+
 def _use_contrib(V, kind, owner) -> bool:
     """Block-owner gather (fa_plan_contrib) for linear elasticity on P1/P2 triangles and
     tetrahedra. owner=None (default) uses it for triangles, where it measured faster (config A
@@ -639,14 +658,15 @@ def _plan_contrib(V, fm, adj, fb, rs, plan, sh):
 
 def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.FA_LINEAR_ELASTICITY,
                 deterministic: bool = False, owner: bool | None = None, slots: bool = True,
-                order: str = "positional", locality: bool = True, search: bool = False):
+                order: str = "positional", locality: bool = True, search: bool = False, stage: bool = True):
     """Row-chunk plan of the gather kernel of a form kind for one row part of A's pattern (cached
     on V per options). Neo-Hookean forms get their own chunking (fa_plan_gather_form); the other
     kinds share one. deterministic: the LDS-atomic gather's plan (no contribution plan), for
     FA_DETERMINISTIC. owner: the block-owner contribution plan (None: for triangles). slots: the
     per-entry slot map (fa_plan_slots; False: the kernels search the pattern in LDS). order: the
     slot map's LDS order (_plan_order). search: the order's alternating-path moves (opt-in).
-    locality: the chunk visiting order (fa_plan_locality: Morton order, walked per XCD)."""
+    locality: the chunk visiting order (fa_plan_locality: Morton order, walked per XCD). stage
+    (neo-Hookean): the chunks' cell lists (fa_plan_cells), so the gather stages cell records in LDS."""
     if deterministic and owner:
         raise ValueError("deterministic assembly runs the LDS-atomic gather: owner=True (block-owner plan) "
                          "cannot be combined with deterministic=True")
@@ -655,7 +675,8 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.
         raise ValueError("the neo-Hookean gather needs positional plans (slots=True, order='positional')")
     plans = V.__dict__.setdefault("_plans", {})
     contrib = _use_contrib(V, kind, owner) and not deterministic
-    key = (A.indptr.data_ptr(), A.parts[part][0], A.parts[part][1], neo, contrib, slots, order, locality, search)
+    key = (A.indptr.data_ptr(), A.parts[part][0], A.parts[part][1], neo, contrib, slots, order, locality, search,
+           stage and neo)
     if key not in plans:
         L = _lib.load()
         fm = V._fa_mesh()
@@ -684,7 +705,8 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.
             # same column split, the neo-Hookean gather)
             eadj = _plan_order(V, fm, adj, fb, plan, sh, order=order, search=search)
         corder = _plan_locality(V, fm, adj, plan, sh, locality)
-        plans[key] = (plan, rs, A.indptr, smap, eadj, corder)
+        cells = _plan_cells(V, fm, adj, fb, plan, sh) if neo and stage and eadj is not None else None
+        plans[key] = (plan, rs, A.indptr, smap, eadj, corder, cells)
         V.__dict__.setdefault("_plan_xver", {})[key] = _coords_version(V.mesh)
     plan = plans[key][0]
     _recheck_affine(V, key, plan)

@@ -13,6 +13,7 @@ by spin kernels), whose duration matches the real exchange's, beside the interio
 usage: python tools/overlap_probe.py [--n 203] [--rank 3] [--world 8] [--reps 10] [--link-GBps 70]
 """
 import argparse
+import ctypes
 import json
 import os
 import statistics
@@ -48,6 +49,9 @@ def main():
     ap.add_argument("--link-GBps", dest="link_GBps", type=float, default=70.0,
                     help="paced transfer rate: one xGMI link direction (~153 GB/s per link both ways; ~64-76 GB/s one way)")
     ap.add_argument("--pieces", type=int, default=64)
+    ap.add_argument("--cu-masks", default="",
+                    help="round 6: comma list of CU masks for the interior rows / the transfer, e.g. c1,s1,s2,s4 "
+                         "(c: bits 0..8k-1 left out, s: k bits of every 32-bit mask word)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     out = {"n": args.n, "rank": args.rank, "world": args.world, "form": args.form}
@@ -132,6 +136,62 @@ def main():
         ts.append(e0.elapsed_time(e1))
     out["interior_beside_paced_ms"] = statistics.median(ts)
     out["paced_pieces"], out["link_GBps"] = args.pieces, args.link_GBps
+
+    # Round 6: the transfer given CUs of its own. The interior rows run on a stream
+    # whose CU mask leaves k CUs per XCD out; the paced transfer runs on a stream masked to exactly those
+    # CUs (hipExtStreamCreateWithCUMask). The mask's bit layout (which bit is which XCD's CU) is found by
+    # timing: leaving out bits 0..7 vs one bit in every 32 -- the per-XCD work of the gather is fixed, so
+    # an uneven mask shows as a ~1/3 slower XCD.
+    if args.cu_masks:
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipExtStreamCreateWithCUMask.restype = ctypes.c_int
+        hip.hipExtStreamCreateWithCUMask.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                                      ctypes.POINTER(ctypes.c_uint32)]
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        words = (ncu + 31) // 32
+
+        def masked_stream(bits):
+            arr = (ctypes.c_uint32 * words)()
+            for b in bits:
+                arr[b // 32] |= 1 << (b % 32)
+            h = ctypes.c_void_p()
+            rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), words, arr)
+            if rc != 0:
+                raise RuntimeError(f"hipExtStreamCreateWithCUMask rc={rc}")
+            return torch.cuda.ExternalStream(h.value, device=dev)
+
+        allb = set(range(ncu))
+        res = {}
+        for spec in args.cu_masks.split(","):
+            layout, k = spec[0], int(spec[1:])  # 'c': bits 0..8k-1 left out; 's': k bits per 32-bit word
+            out_bits = set(range(8 * k)) if layout == "c" else {w * 32 + j for w in range(words) for j in range(k)}
+            out_bits &= allb
+            s_int = masked_stream(sorted(allb - out_bits))
+            s_xfer = masked_stream(sorted(out_bits))
+            r = {"cus_left_out": len(out_bits)}
+
+            def interior_masked():
+                s_int.wait_stream(cur)
+                with torch.cuda.stream(s_int):
+                    sg.rows(inner)
+                cur.wait_stream(s_int)
+            r["interior_alone_ms"], _ = timed(interior_masked, args.reps, cur)
+
+            def paced_on(stream):
+                stream.wait_stream(cur)
+                with torch.cuda.stream(stream):
+                    for k2 in range(args.pieces):
+                        dst[k2 * piece:(k2 + 1) * piece].copy_(src[k2 * piece:(k2 + 1) * piece])
+                        torch.cuda._sleep(gap)
+
+            def interior_with_paced_masked():
+                paced_on(s_xfer)
+                interior_masked()
+                cur.wait_stream(s_xfer)
+            r["interior_with_paced_ms"], r["interior_with_paced_min_ms"] = timed(interior_with_paced_masked, args.reps, cur)
+            res[spec] = r
+            print(json.dumps({spec: r}), file=sys.stderr, flush=True)
+        out["cu_mask"] = res
     del prob, sg
     torch.cuda.empty_cache()
     ghost = SlabProblem(args.n, args.rank, args.world, dev, groups=[None] * (args.world - 1), form=args.form,

@@ -20,6 +20,10 @@ def main():
     dev = torch.device("cuda", 0)
     torch.ones(1, device=dev)
     _lib.load()
+    _wm, _wV, _wa, _wb = bench.build_problem(4, dev)  # the library's first launches (code object loading)
+    fem.assemble_matrix(_wa, bcs=_wb)
+    torch.cuda.synchronize()
+    del _wm, _wV, _wa, _wb
     out = {}
     t = time.time()
 
@@ -40,8 +44,19 @@ def main():
     mark("bcs_marker")
     V.adjacency()
     mark("adjacency")
+    fm0, adj0 = V._fa_mesh(), V._fa_adjacency()
+    indptr = torch.empty(V.num_nodes + 1, dtype=torch.int64, device=dev)
+    nb = ctypes.c_int64(0)
+    Lb = _lib.load()
+    sh0 = _lib.stream_handle(dev)
+    _lib.check(Lb.fa_sparsity_count(ctypes.byref(fm0), ctypes.byref(adj0), indptr.data_ptr(), ctypes.byref(nb), sh0), "count")
+    mark("sparsity_count")
+    indices = torch.empty(nb.value, dtype=torch.int32, device=dev)
+    _lib.check(Lb.fa_sparsity_fill(ctypes.byref(fm0), ctypes.byref(adj0), indptr.data_ptr(), indices.data_ptr(), sh0), "fill")
+    mark("sparsity_fill")
+    V._pattern = (indptr, indices)
     A = fem.create_matrix(a)
-    mark("sparsity")
+    mark("matrix_alloc")
     L = _lib.load()
     fm, adj, fb = V._fa_mesh(), V._fa_adjacency(), fem._fa_bsr(A, 0)
     rs = torch.empty(A.parts[0][1] - A.parts[0][0] + 1, dtype=torch.int64, device=dev)
