@@ -1410,9 +1410,7 @@ static constexpr int kGatherLdsValues = FA_GATHER_LDS;  // accumulator bytes per
 // neo-Hookean gather (2 workgroups / CU, VGPR-bound): a larger accumulator, and chunks capped at
 // 256 / NSPLIT adjacency entries so one chunk's items fill the workgroup's 256 lanes once
 // (fa_plan_gather_form); with the default plan ~96 entries -> 192 items left a wave idle
-// (round 6: 41,472 = 576 blocks, so that the staged cell records (k_gather_neo<STG>) fit beside it at
-// 2 workgroups / CU; the neo plans' chunks are entry-bound at ~120 entries either way)
-constexpr int FA_GATHER_LDS_NEO = 41472;
+constexpr int FA_GATHER_LDS_NEO = 46080;
 static constexpr int kGatherLdsNeo = FA_GATHER_LDS_NEO;
 constexpr int FA_NEO_NSPLIT = 2;  // neo-Hookean column items of 5 columns (E-neo at 2 waves / SIMD, round 2: NSPLIT 2
                                   // 342 ms, 5 at 3 waves 349, 10 at 4 waves 461; round 5: whole entries, 256
@@ -1515,11 +1513,6 @@ struct GatherArgs {
   const int64_t* cw;       // [nchunks + 1] offsets of the chunks' word sections (u16 units)
   const int32_t* ccells;   // [nchunks][FA_OWN_CCAP] the chunk's distinct cells (-1 padded)
   const uint16_t* cwords;  // per chunk: 256 lane starts, then K x 256 contribution words
-  // neo-Hookean chunk cell lists (fa_plan_cells) or NULL: each chunk's distinct cells at its first
-  // entries (ncell), each position's index in that list (nslot); k_gather_neo<STG> stages the
-  // chunk's cell records in LDS
-  const int32_t* ncell;
-  const uint8_t* nslot;
 };
 
 // The record of cell c for the gather (all kinds but the neo-Hookean tangents): see Rec.
@@ -3175,13 +3168,7 @@ __global__ __launch_bounds__(256, 3) void k_neo_records_m(MeshView M, FormView F
 }
 
 // 2 waves / SIMD (215 VGPRs, no spills in the item loop; 3 waves measured slower: spilled records)
-// STG (round 6, plans with fa_plan_cells' lists): the records of a chunk's distinct cells are staged in
-// LDS by the whole workgroup with coalesced 16-B loads -- each cell's record once, as ~24 lanes of one
-// wave instruction -- one chunk ahead (issued after the items, written after the drain), and every
-// item reads its cell's record from LDS. Without STG every item loads its own cell's 376-B record with
-// scattered 16-B loads (two items per entry, ~1.6 entries per cell per chunk: each record fetched ~3
-// times, 24 load instructions of ~32 cache lines each per lane).
-template <int GD, int NN, int NQ, int NSPLIT, bool STG = false>
+template <int GD, int NN, int NQ, int NSPLIT>
 __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint32_t* __restrict__ zero32,
                                                        double* __restrict__ dump, int64_t per) {
   using R = NeoM<GD, NQ>;
@@ -3200,12 +3187,6 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
   __shared__ __attribute__((aligned(16))) double acc[2 * NP2];
   __shared__ __attribute__((aligned(16))) double s_phi[NN * NQ * GD];  // [b][q][k]: a column's gradients at every point, contiguous
   __shared__ __attribute__((aligned(16))) double s_T[NN * NN * NT];    // [a][b][t]
-  // STG: the chunk's cell records ([slot][head | points], padded to RSTR doubles: 4 banks apart) and
-  // the cell lists of the chunks of both parities ahead (-1 past a chunk's last cell)
-  constexpr int CCAP = FA_NEO_CELL_CAP, NPC = R::SIZE / 2, RSTR = R::SIZE + 2;
-  constexpr int NRS = (CCAP * NPC + 255) / 256;  // staged 16-B pieces per lane
-  __shared__ __attribute__((aligned(16))) double s_rec[STG ? CCAP * RSTR : 2];
-  __shared__ int32_t s_cl[STG ? 2 * CCAP : 1];
   dv2* acc2 = reinterpret_cast<dv2*>(acc);
   const int tid = threadIdx.x;
   // chunk schedule of k_gather_lin (round 5): the resident grid pulls chunks from 8 per-XCD counters,
@@ -3271,15 +3252,9 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
   auto load_entry = [&](const Desc& d) -> int32_t { return eadj[entry_of(d)]; };
   // the head's S and s_c (NT + 1 values; its padding is not loaded); slots two per register
   constexpr int HL = NT + 1, NSL = (NBG + 1) / 2;
-  struct Item { double hd[HL]; double pt[NQL][R::PT]; uint32_t sl[NSL]; uint32_t mask; uint32_t cs; };
+  struct Item { double hd[HL]; double pt[NQL][R::PT]; uint32_t sl[NSL]; uint32_t mask; };
   auto load_item = [&](const Desc& d, int32_t pflat, Item& it) {
     const int64_t c = pflat / NN;
-    if constexpr (STG) {  // the record comes from the staged cells (stage_* below): its slot only
-      load_slot_words<NN, NSPLIT>(P.slots, entry_of(d), part, it.sl);
-      it.mask = mk[c * mkmul] * mkmul;
-      it.cs = P.nslot[entry_of(d)];
-      return;
-    }
     const double* hq = P.rec + R::head(c);
     const dv2* hp = reinterpret_cast<const dv2*>(hq);
 #pragma unroll
@@ -3302,72 +3277,10 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
     load_slot_words<NN, NSPLIT>(P.slots, entry_of(d), part, it.sl);
     it.mask = mk[c * mkmul] * mkmul;
   };
-  // STG: a chunk's cell list (lane t < CCAP: its t-th cell, -1 past the last) and its records, piece
-  // f = tid + 256 r of the staging = cell f / NPC, 16-B piece f % NPC of [head | points]
-  auto list_load = [&](const Desc& d) -> int32_t {
-    return (tid < CCAP && tid < d.na) ? P.ncell[d.a0 + tid] : -1;
-  };
-  // (the lane's piece indices are recomputed at every use from an opaque copy of tid: hoisted out of the
-  // chunk loop they were 16 registers live through the items, and spilled)
-  auto stage_load = [&](int par, dv2 (&g)[NRS]) {
-    int t0 = tid;
-    asm volatile("" : "+v"(t0));
-#pragma unroll
-    for (int r = 0; r < NRS; ++r) {
-      const int f = t0 + 256 * r, i = min(f / NPC, CCAP - 1), j = f % NPC;
-      int32_t c = s_cl[par * CCAP + i];
-      c = c >= 0 ? c : max(s_cl[par * CCAP], 0);  // (past the list: any valid record; not written)
-      // NeoM tiles: [64 heads][point 0: 64 x PT] ..., cell c at tile c >> 6, lane c & 63
-      const bool hd = j < R::HEAD / 2;
-      const int jq = (j - R::HEAD / 2) / (R::PT / 2), jk = (j - R::HEAD / 2) % (R::PT / 2);
-      const int in_tile = hd ? (c & 63) * R::HEAD + 2 * j : 64 * R::HEAD + jq * (64 * R::PT) + (c & 63) * R::PT + 2 * jk;
-      g[r] = *reinterpret_cast<const dv2*>(P.rec + (int64_t)(c >> 6) * (64 * R::SIZE) + in_tile);
-    }
-  };
-  auto stage_store = [&](int par, const dv2 (&g)[NRS]) {
-    int t0 = tid;
-    asm volatile("" : "+v"(t0));
-#pragma unroll
-    for (int r = 0; r < NRS; ++r) {
-      const int f = t0 + 256 * r, i = f / NPC, j = f % NPC;
-      if (i < CCAP && s_cl[par * CCAP + i] >= 0) *reinterpret_cast<dv2*>(s_rec + i * RSTR + 2 * j) = g[r];
-    }
-  };
-  // STG: the item's record from its cell's staged copy
-  auto read_rec = [&](Item& it) {
-    const double* rp = s_rec + min((int)it.cs, CCAP - 1) * RSTR;
-#pragma unroll
-    for (int k = 0; k < HL / 2; ++k) {
-      const dv2 v = *reinterpret_cast<const dv2*>(rp + 2 * k);
-      it.hd[2 * k] = v.x;
-      it.hd[2 * k + 1] = v.y;
-    }
-    if constexpr (HL % 2) it.hd[HL - 1] = rp[HL - 1];
-#pragma unroll
-    for (int ql = 0; ql < NQL; ++ql)
-#pragma unroll
-      for (int k = 0; k < R::PT / 2; ++k) {
-        const dv2 v = *reinterpret_cast<const dv2*>(rp + R::HEAD + ql * R::PT + 2 * k);
-        it.pt[ql][2 * k] = v.x;
-        it.pt[ql][2 * k + 1] = v.y;
-      }
-  };
-
   Desc d0 = desc(0), d1 = desc(1), d2 = desc(2);
   int32_t pf0 = load_entry(d0), pf1 = load_entry(d1);
   Item cur;
   load_item(d0, pf0, cur);
-  if constexpr (STG) {  // chunk 0's records and chunk 1's list staged before the loop
-    if (tid < CCAP) {
-      s_cl[tid] = list_load(d0);
-      s_cl[CCAP + tid] = list_load(d1);
-    }
-    __syncthreads();
-    dv2 g[NRS];
-    stage_load(0, g);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    stage_store(0, g);
-  }
   int bad = 0;
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the prologue's loads (see k_gather_lin)
   __syncthreads();                     // tables and accumulator staged
@@ -3380,7 +3293,6 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
     const int h = (int)(off & 1);
     const int nb = d0.nb;
     const bool valid = jit < d0.na;
-    if constexpr (STG) read_rec(cur);
     {
       const int aloc = pf0 % NN;
       const uint32_t rowm = (cur.mask >> (aloc * GD)) & ((1u << GD) - 1);
@@ -3487,22 +3399,10 @@ __global__ __launch_bounds__(256, 2) void k_gather_neo(GatherArgs P, const uint3
     // chunk k+1's records / slots / masks: the item registers are dead here, and these loads are
     // issued before chunk k's stores (their wait at chunk k+1 does not include the stores)
     load_item(d1, pf1, cur);
-    // STG: chunk k+1's staged records and chunk k+2's cell list, loaded now, written to LDS after the
-    // drain (the items of chunk k have read s_rec by B1)
-    dv2 g[STG ? NRS : 1];
-    int32_t cl2 = -1;
-    if constexpr (STG) {
-      stage_load((k + 1) & 1, g);
-      cl2 = list_load(d2);
-    }
     __syncthreads();  // B1: the chunk is accumulated
     fa_dv2 dv[SW];
     double dh, dt;
     xchg_drain<SW, NTH>(acc, h, nb * BS2, P.A.data + off, tid, dv, dh, dt);
-    if constexpr (STG) {
-      stage_store((k + 1) & 1, g);
-      if (tid < CCAP) s_cl[(k & 1) * CCAP + tid] = cl2;  // parity of k + 2
-    }
     __syncthreads();  // B3: the accumulator is clean for the next chunk's atomics
     keep_vgprs(dv, dh, dt);
     // chunk k + AHEAD's id, read at iteration k + AHEAD - LOOK (after later barriers)
@@ -4116,8 +4016,6 @@ extern "C" int fa_plan_slots(const fa_mesh* mesh, const fa_adjacency* adj, const
   plan->slots = slots;
   plan->slot_order = 0;
   plan->eadj = nullptr;
-  plan->ccell = nullptr;
-  plan->cslot = nullptr;
   return FA_OK;
 }
 
@@ -4379,94 +4277,6 @@ __global__ __launch_bounds__(kPermThreads) void k_plan_perm(const int64_t* __res
   }
 }
 
-// fa_plan_cells: one wave per chunk: the chunk's positional entries' cells (eadj / NN) bitonic-sorted in
-// LDS, the distinct ones listed at ccell[a0 ..), -1 after; every position's index in that list by
-// binary search. Chunks with more than FA_NEO_CELL_CAP cells set *over.
-template <int NN>
-__global__ __launch_bounds__(64) void k_plan_cells(const int64_t* __restrict__ row_start,
-                                                   const int64_t* __restrict__ adj_ptr, const int32_t* __restrict__ eadj,
-                                                   int64_t nchunks, int32_t* __restrict__ ccell,
-                                                   uint8_t* __restrict__ cslot, int* over) {
-  __shared__ int32_t s[kGatherMaxAdj], u[kGatherMaxAdj];
-  const int lane = threadIdx.x;
-  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    const int64_t a0 = adj_ptr[row_start[c]];
-    const int na = (int)min<int64_t>(adj_ptr[row_start[c + 1]] - a0, kGatherMaxAdj);
-    int n2 = 1;
-    while (n2 < na) n2 <<= 1;
-    __syncthreads();
-    for (int t = lane; t < n2; t += 64) s[t] = t < na ? eadj[a0 + t] / NN : INT32_MAX;
-    __syncthreads();
-    for (int k = 2; k <= n2; k <<= 1)
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int t = lane; t < n2; t += 64) {
-          const int x = t ^ j;
-          if (x > t) {
-            const int32_t a = s[t], b = s[x];
-            if ((a > b) == ((t & k) == 0)) { s[t] = b; s[x] = a; }
-          }
-        }
-        __syncthreads();
-      }
-    int nu = 0;
-    for (int t0 = 0; t0 < n2; t0 += 64) {
-      const int t = t0 + lane;
-      const int32_t v = t < n2 ? s[t] : INT32_MAX;
-      const bool keep = v != INT32_MAX && (t == 0 || s[t - 1] != v);
-      const unsigned long long m = __ballot(keep);
-      if (keep) u[nu + __popcll(m & ((1ull << lane) - 1ull))] = v;
-      nu += __popcll(m);
-    }
-    __syncthreads();
-    for (int t = lane; t < na; t += 64) ccell[a0 + t] = t < nu ? u[t] : -1;
-    for (int t = lane; t < na; t += 64) {
-      const int32_t v = eadj[a0 + t] / NN;
-      int lo = 0, hi = nu - 1, f = 0;
-      while (lo <= hi) {
-        const int mid = (lo + hi) >> 1;
-        if (u[mid] == v) { f = mid; break; }
-        if (u[mid] < v) lo = mid + 1; else hi = mid - 1;
-      }
-      cslot[a0 + t] = (uint8_t)min(f, 255);
-    }
-    if (lane == 0 && nu > FA_NEO_CELL_CAP) atomicOr(over, 1);
-  }
-}
-
-extern "C" int fa_plan_cells(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int32_t* ccell,
-                             uint8_t* cslot, fa_plan* plan, void* stream) {
-  int rc = check_mesh(mesh);
-  if (rc) return rc;
-  if (!adj || !A || !ccell || !cslot || !plan) return fail(FA_E_ARG, "null argument");
-  plan->ccell = nullptr;
-  plan->cslot = nullptr;
-  if (!plan->eadj || !plan->row_start || plan->nchunks <= 0) return FA_OK;  // no positional plan: nothing to list
-  if (!(plan->cell_flags & FA_PLAN_NEO)) return FA_OK;  // only the neo-Hookean gather stages cell records
-  hipStream_t s = (hipStream_t)stream;
-  int* over = nullptr;
-  HIP_TRY(hipMallocAsync((void**)&over, sizeof(int), s));
-  HIP_TRY(hipMemsetAsync(over, 0, sizeof(int), s));
-  const int grid = (int)std::min<int64_t>(plan->nchunks, kMaxBlocks);
-  bool ok = true;
-  switch (mesh->nn) {
-    case 10: k_plan_cells<10><<<grid, 64, 0, s>>>(plan->row_start, adj->ptr, plan->eadj, plan->nchunks, ccell, cslot, over); break;
-    case 6: k_plan_cells<6><<<grid, 64, 0, s>>>(plan->row_start, adj->ptr, plan->eadj, plan->nchunks, ccell, cslot, over); break;
-    default: ok = false;
-  }
-  int ho = 1;
-  if (ok) {
-    LAUNCH_CHECK();
-    HIP_TRY(hipMemcpyAsync(&ho, over, sizeof(int), hipMemcpyDeviceToHost, s));
-  }
-  HIP_TRY(hipFreeAsync(over, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  if (ok && !ho) {
-    plan->ccell = ccell;
-    plan->cslot = cslot;
-  }
-  return FA_OK;
-}
-
 // NSPLIT of the affine-simplex linear-elasticity gather kernel for (cell, degree, quadrature
 // points), or 0 when that kernel does not exist (must match dispatch_gather)
 constexpr int FA_P2TET_NSPLIT = 2;  // measured best with the reference-tensor blocks (n=120 sweep)
@@ -4505,8 +4315,6 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   if (!plan->slots) return fail(FA_E_ARG, "fa_plan_order needs the slot map (fa_plan_slots first)");
   plan->slot_order = 0;
   plan->eadj = nullptr;
-  plan->ccell = nullptr;  // cell lists are of a positional order: fa_plan_cells after this
-  plan->cslot = nullptr;
   DevTables T;
   if ((rc = get_tables(mesh->cell_type, mesh->degree, -1, &T))) return rc;
   const int ns = (plan->cell_flags & FA_PLAN_NEO) && is_simplex(mesh->cell_type)
@@ -4735,8 +4543,6 @@ static int plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bs
   plan->eadj = nullptr;
   plan->corder = nullptr;
   plan->contrib = nullptr;
-  plan->ccell = nullptr;
-  plan->cslot = nullptr;
   return FA_OK;
 }
 
@@ -4978,8 +4784,6 @@ extern "C" int fa_plan_contrib(const fa_mesh* mesh, const fa_adjacency* adj, con
 
 // the kernel's views of plan->contrib (NULL pointers without one)
 static void set_contrib(GatherArgs& P, const fa_plan* plan) {
-  P.ncell = plan ? plan->ccell : nullptr;
-  P.nslot = plan && plan->ccell ? plan->cslot : nullptr;
   P.cw = nullptr;
   P.ccells = nullptr;
   P.cwords = nullptr;
@@ -5357,13 +5161,8 @@ static int launch_gather_neo(GatherArgs P, const int8_t* bc, hipStream_t s, cons
     if ((rc = lin_scratch(&zero32, &dump))) return rc;
     int64_t* ldesc = nullptr;
     if ((rc = lin_chunk_desc(P, &ldesc, s, P.corder))) return rc;
-    if (P.ncell && P.nslot) {  // chunk cell lists (fa_plan_cells): records staged per chunk in LDS
-      const int64_t grid = gather_grid(k_gather_neo<GD, NN, NQ, NSPLIT, true>, P.nchunks, 256);
-      k_gather_neo<GD, NN, NQ, NSPLIT, true><<<(unsigned)grid, 256, 0, s>>>(P, zero32, dump, (P.nchunks + 7) / 8);
-    } else {
-      const int64_t grid = gather_grid(k_gather_neo<GD, NN, NQ, NSPLIT>, P.nchunks, 256);
-      k_gather_neo<GD, NN, NQ, NSPLIT><<<(unsigned)grid, 256, 0, s>>>(P, zero32, dump, (P.nchunks + 7) / 8);
-    }
+    const int64_t grid = gather_grid(k_gather_neo<GD, NN, NQ, NSPLIT>, P.nchunks, 256);
+    k_gather_neo<GD, NN, NQ, NSPLIT><<<(unsigned)grid, 256, 0, s>>>(P, zero32, dump, (P.nchunks + 7) / 8);
     LAUNCH_CHECK();
     HIP_TRY(hipFreeAsync(ldesc, s));
     if (bc) {  // Dirichlet diagonals (dolfinx set_diagonal) of the plan's rows

@@ -18,7 +18,6 @@ FA_TRIANGLE, FA_QUADRILATERAL, FA_TETRAHEDRON, FA_HEXAHEDRON = 3, 4, -4, 8
 FA_LINEAR_ELASTICITY, FA_ASYM_DAMAGE, FA_NEO_HOOKEAN, FA_ASYM_DAMAGE_AD = 0, 1, 2, 3
 FA_GATHER, FA_SCATTER, FA_ZERO_FIRST, FA_DETERMINISTIC, FA_CHECK_ERRORS = 0x0, 0x1, 0x2, 0x4, 0x8
 FA_PLAN_AFFINE, FA_PLAN_DETERMINISTIC, FA_PLAN_ORDER_SEARCH, FA_PLAN_NEO = 0x1, 0x2, 0x4, 0x8
-FA_NEO_CELL_CAP = 82  # cells per chunk the staged neo-Hookean gather holds (fa_plan_cells)
 
 
 class FemasmError(RuntimeError):
@@ -85,8 +84,6 @@ class fa_plan(ctypes.Structure):
         ("eadj", ctypes.c_void_p),
         ("corder", ctypes.c_void_p),
         ("contrib", ctypes.c_void_p),
-        ("ccell", ctypes.c_void_p),
-        ("cslot", ctypes.c_void_p),
     ]
 
 
@@ -111,7 +108,6 @@ SIGNATURES = {
     "fa_plan_gather_contrib": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_plan_contrib_bytes": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_plan_contrib": (ctypes.c_int, [P, P, P, P, I64, P, P]),
-    "fa_plan_cells": (ctypes.c_int, [P, P, P, P, P, P, P]),
     "fa_tabulate_cells": (ctypes.c_int, [P, P, I64, I64, P, P]),
     "fa_assemble_matrix": (ctypes.c_int, [P, P, P, P, P, D, P, I32, P]),
     "fa_gather_work_bytes": (ctypes.c_int, [P, P, P]),

@@ -609,19 +609,6 @@ def _plan_locality(V, fm, adj, plan, sh, locality: bool = True):
     return corder if plan.corder else None
 
 
-def _plan_cells(V, fm, adj, fb, plan, sh):
-    """Each chunk's distinct cells and every position's index among them (fa_plan_cells): the neo-Hookean
-    gather then stages the chunk's cell records in LDS with coalesced loads. Returns the buffers (kept
-    with the plan), or None when a chunk has more cells than the kernel's staging holds (the gather then
-    loads every item's record itself)."""
-    nent = V.mesh.num_cells * V.nn
-    ccell = torch.empty(max(nent, 1), dtype=torch.int32, device=V.mesh.device)
-    cslot = torch.empty(max(nent, 1), dtype=torch.uint8, device=V.mesh.device)
-    _lib.check(_lib.load().fa_plan_cells(ctypes.byref(fm), ctypes.byref(adj), ctypes.byref(fb), ccell.data_ptr(),
-                                         cslot.data_ptr(), ctypes.byref(plan), sh), "fa_plan_cells")
-    return (ccell, cslot) if plan.ccell else None
-
-
 def _use_contrib(V, kind, owner) -> bool:
     """Block-owner gather (fa_plan_contrib) for linear elasticity on P1/P2 triangles and
     tetrahedra. owner=None (default) uses it for triangles, where it measured faster (config A
@@ -658,15 +645,14 @@ def _plan_contrib(V, fm, adj, fb, rs, plan, sh):
 
 def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.FA_LINEAR_ELASTICITY,
                 deterministic: bool = False, owner: bool | None = None, slots: bool = True,
-                order: str = "positional", locality: bool = True, search: bool = False, stage: bool = True):
+                order: str = "positional", locality: bool = True, search: bool = False):
     """Row-chunk plan of the gather kernel of a form kind for one row part of A's pattern (cached
     on V per options). Neo-Hookean forms get their own chunking (fa_plan_gather_form); the other
     kinds share one. deterministic: the LDS-atomic gather's plan (no contribution plan), for
     FA_DETERMINISTIC. owner: the block-owner contribution plan (None: for triangles). slots: the
     per-entry slot map (fa_plan_slots; False: the kernels search the pattern in LDS). order: the
     slot map's LDS order (_plan_order). search: the order's alternating-path moves (opt-in).
-    locality: the chunk visiting order (fa_plan_locality: Morton order, walked per XCD). stage
-    (neo-Hookean): the chunks' cell lists (fa_plan_cells), so the gather stages cell records in LDS."""
+    locality: the chunk visiting order (fa_plan_locality: Morton order, walked per XCD)."""
     if deterministic and owner:
         raise ValueError("deterministic assembly runs the LDS-atomic gather: owner=True (block-owner plan) "
                          "cannot be combined with deterministic=True")
@@ -675,8 +661,7 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.
         raise ValueError("the neo-Hookean gather needs positional plans (slots=True, order='positional')")
     plans = V.__dict__.setdefault("_plans", {})
     contrib = _use_contrib(V, kind, owner) and not deterministic
-    key = (A.indptr.data_ptr(), A.parts[part][0], A.parts[part][1], neo, contrib, slots, order, locality, search,
-           stage and neo)
+    key = (A.indptr.data_ptr(), A.parts[part][0], A.parts[part][1], neo, contrib, slots, order, locality, search)
     if key not in plans:
         L = _lib.load()
         fm = V._fa_mesh()
@@ -705,8 +690,7 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.
             # same column split, the neo-Hookean gather)
             eadj = _plan_order(V, fm, adj, fb, plan, sh, order=order, search=search)
         corder = _plan_locality(V, fm, adj, plan, sh, locality)
-        cells = _plan_cells(V, fm, adj, fb, plan, sh) if neo and stage and eadj is not None else None
-        plans[key] = (plan, rs, A.indptr, smap, eadj, corder, cells)
+        plans[key] = (plan, rs, A.indptr, smap, eadj, corder)
         V.__dict__.setdefault("_plan_xver", {})[key] = _coords_version(V.mesh)
     plan = plans[key][0]
     _recheck_affine(V, key, plan)

@@ -155,9 +155,6 @@ typedef struct {
   const void* contrib;       /* optional contribution plan (fa_plan_contrib): P1/P2 simplices with
                                 linear elasticity of one Poisson ratio then assemble through the
                                 block-owner gather (no per-contribution LDS atomics) */
-  const int32_t* ccell;      /* optional (fa_plan_cells, neo-Hookean positional plans): each chunk's
-                                distinct cells, ccell[a0 .. a0 + n) ascending, -1 up to its last entry */
-  const uint8_t* cslot;      /* with ccell: per position, the index of its cell in its chunk's list */
 } fa_plan;
 
 const char* fa_last_error(void);
@@ -235,18 +232,6 @@ int fa_plan_check_affine(const fa_mesh* mesh, fa_plan* plan, void* stream);
  * buffer of plan->nchunks int32; on success plan->corder points to it. Any permutation assembles
  * the same matrix (each chunk owns its rows); only the re-reads of the records change. */
 int fa_plan_locality(const fa_mesh* mesh, const fa_adjacency* adj, int32_t* corder, fa_plan* plan, void* stream);
-
-/* Cell lists of a neo-Hookean positional plan (after fa_plan_order with an entry buffer on a plan of
- * fa_plan_gather_form(FA_NEO_HOOKEAN)): for each chunk, whose adjacency entries are positions
- * [a0, a0 + na) of plan->eadj, its distinct cells in ascending order at ccell[a0 .. a0 + n) and -1 at
- * ccell[a0 + n .. a0 + na); cslot[p] = the index of position p's cell in that list. ccell (int32) and
- * cslot (uint8) are caller-owned device buffers of ncells * nn entries. When every chunk has at most
- * FA_NEO_CELL_CAP cells, sets plan->ccell / plan->cslot: the neo-Hookean gather then stages each
- * chunk's cell records in LDS with coalesced loads instead of every item loading its cell's record
- * (config E-neo); otherwise leaves them NULL (the gather loads per item). Synchronises `stream`. */
-#define FA_NEO_CELL_CAP 82
-int fa_plan_cells(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, int32_t* ccell, uint8_t* cslot,
-                  fa_plan* plan, void* stream);
 
 /* Block-owner gather (P1/P2 triangles and tetrahedra, linear elasticity with one Poisson ratio).
  * fa_plan_gather_contrib chunks the rows for it (like fa_plan_gather, smaller chunks: at most

@@ -144,30 +144,3 @@ def test_neohookean_needs_positional_plan(oracle, dev, order):
                               ctypes.byref(plan), None, 1.0, ctypes.byref(A._fa_bsr(0)), _lib.FA_GATHER,
                               _lib.stream_handle(dev))
     assert rc == -1 and "positional plan" in L.fa_last_error().decode()
-
-
-@pytest.mark.parametrize("ct,p,n", [(-4, 2, (6, 5, 7)), (3, 2, (30, 23)), (-4, 2, (3, 2, 2))])
-def test_neohookean_staged_records(oracle, dev, ct, p, n):
-    """Round 6: a neo-Hookean plan with chunk cell lists (fa_plan_cells) makes the gather stage each
-    chunk's cell records in LDS; without them every item loads its own. Both meet the per-row bar
-    against the oracle and each other, with bcs, over many chunks."""
-    from femasm import fem
-    from rowparity import assert_rows_close
-
-    m, V, a = _setup(oracle, ct, p, n, dev)
-    left = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
-    bcs = [fem.dirichletbc(0.0, left, V)]
-    A = fem.create_matrix(a)
-    plan = fem.gather_plan(V, A, 0, a.kind)
-    assert plan.ccell and plan.cslot, "the default neo plan carries cell lists"
-    fem.assemble_matrix(a, bcs=bcs, A=A)
-    staged = A.data.clone()
-    fem.assemble_matrix(a, bcs=bcs, A=A, plan={"stage": False})
-    loaded = A.data.clone()
-    marker, _ = fem._combine_bcs(V, bcs)
-    indptr, indices = oracle.sparsity(_np(V.dofmap), V.num_nodes)
-    lam, mu = oracle.lame(_np(a.E), 0.3)
-    ref = oracle.assemble_neohookean(int(m.cell_type), p, _np(V.dofmap), _np(m.cells), _np(m.x), lam, mu, _np(a.u),
-                                     indptr, indices, bc=_np(marker), diag=1.0, qdeg=a.qdeg)
-    assert_rows_close(_np(staged), ref, indptr, RTOL)
-    assert_rows_close(_np(loaded), ref, indptr, RTOL)
