@@ -3719,64 +3719,130 @@ extern "C" int fa_build_adjacency(const fa_mesh* mesh, int64_t* ptr, int32_t* id
 // ------------------------------------------------------------------------------------ sparsity
 static constexpr int kSparsityCap = 2048;  // candidate (cell, node) pairs per row
 
-// One 64-thread workgroup (one wave) per row: gather the nodes of the row's adjacent cells,
-// bitonic-sort them in LDS, keep the unique ones. PASS 0 counts, PASS 1 fills.
+// One 64-thread workgroup (one wave) per row: the nodes of the row's adjacent cells go into an LDS
+// hash set (open addressing, kSparsityHash slots); its occupied slots are compacted to the row's
+// distinct columns. PASS 0 counts them. PASS 1 sorts them: up to 64 in registers (a bitonic network
+// over the wave's lanes, one value per lane), more in LDS (bitonic), and writes them. (Round 6: the
+// candidates -- ~74 per row of config E -- were bitonic-sorted in LDS in both passes, 0.27 s.)
+constexpr int kSparsityHash = 1024;  // > 2 x the distinct columns of a row the hash takes (else the LDS sort)
+__device__ __forceinline__ uint32_t sp_hash(int32_t v) { return ((uint32_t)v * 0x9E3779B1u) >> (32 - 10); }
 template <int PASS>
 __global__ __launch_bounds__(64) void k_sparsity(MeshView M, const int64_t* __restrict__ adj_ptr,
                                                  const int32_t* __restrict__ adj_idx, int64_t* __restrict__ counts,
                                                  const int64_t* __restrict__ indptr, int32_t* __restrict__ indices,
                                                  int* err) {
+  static_assert(kSparsityHash == 1024, "sp_hash: 10 bits");
   __shared__ int32_t s[kSparsityCap];
+  __shared__ int32_t h[kSparsityHash];
   const int lane = threadIdx.x;
   const int nn = M.nn;
   for (int64_t r = blockIdx.x; r < M.nnodes; r += gridDim.x) {
-  __syncthreads();
   const int64_t j0 = adj_ptr[r], j1 = adj_ptr[r + 1];
   const int64_t ncand = (j1 - j0) * nn;
   if (ncand > kSparsityCap) {
     if (lane == 0) atomicOr(err, 4);
     continue;
   }
-  int n2 = 1;
-  while (n2 < ncand) n2 <<= 1;
-  for (int t = lane; t < n2; t += 64) {
-    int32_t v = 0x7fffffff;
-    if (t < ncand) {
-      int32_t p = adj_idx[j0 + t / nn];
-      int64_t c = p / nn;
-      v = M.cells[c * nn + t % nn];
+  __syncthreads();  // the previous row's reads of h / s are done
+  auto bitonic = [&](int n2) {  // s[0, n2) ascending (n2 a power of two)
+    for (int k = 2; k <= n2; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int t = lane; t < n2; t += 64) {
+          const int ixj = t ^ j;
+          if (ixj > t) {
+            const int32_t a = s[t], b = s[ixj];
+            if ((a > b) == ((t & k) == 0)) { s[t] = b; s[ixj] = a; }
+          }
+        }
+        __syncthreads();
+      }
+  };
+  if (ncand >= kSparsityHash / 2) {  // long rows (high-order hexahedra): sort the candidates, keep the unique
+    int n2 = 1;
+    while (n2 < ncand) n2 <<= 1;
+    for (int t = lane; t < n2; t += 64)
+      s[t] = t < ncand ? M.cells[(int64_t)(adj_idx[j0 + t / nn] / nn) * nn + t % nn] : INT32_MAX;
+    __syncthreads();
+    bitonic(n2);
+    const int64_t base = PASS ? indptr[r] : 0;
+    int running = 0;
+    for (int t0 = 0; t0 < n2; t0 += 64) {
+      const int t = t0 + lane;
+      const int32_t v = t < n2 ? s[t] : INT32_MAX;
+      const bool keep = v != INT32_MAX && (t == 0 || s[t - 1] != v);
+      const unsigned long long m = __ballot(keep);
+      if (PASS && keep) indices[base + running + __popcll(m & ((1ull << lane) - 1ull))] = v;
+      running += __popcll(m);
     }
-    s[t] = v;
+    if (!PASS && lane == 0) counts[r] = running;
+    continue;
+  }
+  for (int t = lane; t < kSparsityHash; t += 64) h[t] = -1;
+  __syncthreads();
+  for (int t = lane; t < ncand; t += 64) {
+    const int32_t v = M.cells[(int64_t)(adj_idx[j0 + t / nn] / nn) * nn + t % nn];
+    uint32_t k = sp_hash(v);
+    for (;;) {  // terminates: fewer than kSparsityHash / 2 values go into the table
+      const int32_t prev = atomicCAS(&h[k], -1, v);
+      if (prev == -1 || prev == v) break;
+      k = (k + 1) & (kSparsityHash - 1);
+    }
   }
   __syncthreads();
-  for (int k = 2; k <= n2; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = lane; t < n2; t += 64) {
-        int ixj = t ^ j;
-        if (ixj > t) {
-          int32_t x = s[t], y = s[ixj];
-          bool up = (t & k) == 0;
-          if ((x > y) == up) { s[t] = y; s[ixj] = x; }
+  // compaction of the occupied slots (in hash order)
+  int u = 0;
+  for (int t0 = 0; t0 < kSparsityHash; t0 += 64) {
+    const int32_t v = h[t0 + lane];
+    const bool keep = v >= 0;
+    const unsigned long long m = __ballot(keep);
+    if (PASS && keep) s[u + __popcll(m & ((1ull << lane) - 1ull))] = v;
+    u += __popcll(m);
+  }
+  if (!PASS) {
+    if (lane == 0) counts[r] = u;
+    continue;
+  }
+  __syncthreads();
+  const int64_t base = indptr[r];
+  if (u <= 64) {  // one value per lane, bitonic across the wave (padding sorts last)
+    int32_t x = lane < u ? s[lane] : INT32_MAX;
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const int32_t y = __shfl_xor(x, j);
+        const bool up = (lane & k) == 0, lo = (lane & j) == 0;
+        x = (lo == up) ? min(x, y) : max(x, y);
+      }
+    if (lane < u) indices[base + lane] = x;
+  } else if (u <= 128) {  // two per lane (elements lane and lane + 64; config E's vertex rows hold ~65)
+    int32_t x0 = s[lane], x1 = 64 + lane < u ? s[64 + lane] : INT32_MAX;
+#pragma unroll
+    for (int k = 2; k <= 128; k <<= 1)
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        if (j == 64) {  // partners in one lane (k = 128: ascending)
+          const int32_t a = min(x0, x1), b = max(x0, x1);
+          x0 = a;
+          x1 = b;
+        } else {
+          const bool lo = (lane & j) == 0;
+          const bool up0 = (lane & k) == 0, up1 = ((64 + lane) & k) == 0;
+          const int32_t y0 = __shfl_xor(x0, j), y1 = __shfl_xor(x1, j);
+          x0 = (lo == up0) ? min(x0, y0) : max(x0, y0);
+          x1 = (lo == up1) ? min(x1, y1) : max(x1, y1);
         }
       }
-      __syncthreads();
-    }
-  int64_t base = PASS ? indptr[r] : 0;
-  int running = 0;
-  for (int t0 = 0; t0 < n2; t0 += 64) {
-    int t = t0 + lane;
-    bool keep = false;
-    int32_t v = 0;
-    if (t < n2) {
-      v = s[t];
-      keep = (v != 0x7fffffff) && (t == 0 || s[t - 1] != v);
-    }
-    unsigned long long m = __ballot(keep);
-    int rank = __popcll(m & ((1ull << lane) - 1ull));
-    if (PASS && keep) indices[base + running + rank] = v;
-    running += __popcll(m);
+    indices[base + lane] = x0;  // u > 64
+    if (64 + lane < u) indices[base + 64 + lane] = x1;
+  } else {
+    int n2 = 1;
+    while (n2 < u) n2 <<= 1;
+    for (int t = u + lane; t < n2; t += 64) s[t] = INT32_MAX;
+    __syncthreads();
+    bitonic(n2);
+    for (int t = lane; t < u; t += 64) indices[base + t] = s[t];
   }
-  if (!PASS && lane == 0) counts[r] = running;
   }
 }
 
