@@ -645,18 +645,23 @@ def _plan_contrib(V, fm, adj, fb, rs, plan, sh):
 
 def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.FA_LINEAR_ELASTICITY,
                 deterministic: bool = False, owner: bool | None = None, slots: bool = True,
-                order: str = "positional", locality: bool = True, search: bool = False):
+                order: str = "positional", locality: bool | None = None, search: bool = False):
     """Row-chunk plan of the gather kernel of a form kind for one row part of A's pattern (cached
     on V per options). Neo-Hookean forms get their own chunking (fa_plan_gather_form); the other
     kinds share one. deterministic: the LDS-atomic gather's plan (no contribution plan), for
     FA_DETERMINISTIC. owner: the block-owner contribution plan (None: for triangles). slots: the
     per-entry slot map (fa_plan_slots; False: the kernels search the pattern in LDS). order: the
     slot map's LDS order (_plan_order). search: the order's alternating-path moves (opt-in).
-    locality: the chunk visiting order (fa_plan_locality: Morton order, walked per XCD)."""
+    locality: the chunk visiting order (fa_plan_locality: Morton order, walked per XCD); None (default):
+    Morton order for the neo-Hookean gather (its 384-B records: 106.5 -> 56.4 GB fetched per launch,
+    round 5), row order for the others (config E: 35.8 vs 36.3, 36.0 vs 36.2, 35.13 vs 35.29 ms on three
+    boxes; C 0.99 vs 1.01 ms)."""
     if deterministic and owner:
         raise ValueError("deterministic assembly runs the LDS-atomic gather: owner=True (block-owner plan) "
                          "cannot be combined with deterministic=True")
     neo = kind == _lib.FA_NEO_HOOKEAN
+    if locality is None:
+        locality = neo
     if neo and not (slots and order == "positional"):
         raise ValueError("the neo-Hookean gather needs positional plans (slots=True, order='positional')")
     plans = V.__dict__.setdefault("_plans", {})
@@ -807,7 +812,8 @@ class SplitGather:
             self.plans.append(plan)
             self._keep.append(rs)
             if r1 > r0:
-                self._keep.append(_plan_locality(V, self.fm, self.adj, plan, self.sh))
+                self._keep.append(_plan_locality(V, self.fm, self.adj, plan, self.sh,
+                                                 locality=a.kind == _lib.FA_NEO_HOOKEAN))  # (gather_plan's default)
         if self.slots is not None:
             # one slot map for all rows (fa_plan_slots writes every row), then each plan's order
             live = [i for i, (r0, r1) in enumerate(ranges) if r1 > r0]
