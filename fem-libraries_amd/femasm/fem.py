@@ -597,12 +597,24 @@ def _plan_order(V, fm, adj, fb, plan, sh, eadj=None, order: str = "positional", 
     return eadj if plan.eadj else None
 
 
-def _plan_locality(V, fm, adj, plan, sh, locality: bool = True):
-    """Chunk visiting order of the gather (fa_plan_locality): Morton order of the chunks' positions,
-    so chunks that share cells run close in time and the cells' records are re-read from L2, not
-    HBM. locality=False keeps row order."""
-    if not locality or plan.nchunks <= 1:
+def _plan_locality(V, fm, adj, plan, sh, locality=True):
+    """Chunk visiting order of the gather (the kernels' XCD x walks positions [x per, (x + 1) per) of
+    it). True / "morton": fa_plan_locality, Morton order of the chunks' positions, so chunks that share
+    cells run close in time on one XCD and the cells' records are re-read from its L2. "deal": row
+    order dealt to the XCDs in pairs of chunks (chunk c to XCD (c // 2) mod 8): every XCD works in one
+    compact window of the matrix at any time (the neo-Hookean gather, round 6: 62.1-62.2 vs 63.2-63.3 ms
+    Morton on config E-neo, profiles/r6/order_variants_Eneo.txt). False / "row": row order, XCD x
+    taking the contiguous eighth x of the chunks."""
+    if locality in (False, "row") or plan.nchunks <= 1:
         return None
+    if locality == "deal":
+        nch = int(plan.nchunks)
+        c = torch.arange(nch, device=V.mesh.device, dtype=torch.int64)
+        corder = torch.argsort(((c // 2) % 8) * nch + c).to(torch.int32).contiguous()
+        plan.corder = corder.data_ptr()
+        return corder
+    if locality not in (True, "morton"):
+        raise ValueError(f"unknown chunk order {locality!r}")
     corder = torch.empty(plan.nchunks, dtype=torch.int32, device=V.mesh.device)
     _lib.check(_lib.load().fa_plan_locality(ctypes.byref(fm), ctypes.byref(adj), corder.data_ptr(),
                                             ctypes.byref(plan), sh), "fa_plan_locality")
@@ -652,16 +664,16 @@ def gather_plan(V: FunctionSpace, A: MatrixCSR, part: int = 0, kind: int = _lib.
     FA_DETERMINISTIC. owner: the block-owner contribution plan (None: for triangles). slots: the
     per-entry slot map (fa_plan_slots; False: the kernels search the pattern in LDS). order: the
     slot map's LDS order (_plan_order). search: the order's alternating-path moves (opt-in).
-    locality: the chunk visiting order (fa_plan_locality: Morton order, walked per XCD); None (default):
-    Morton order for the neo-Hookean gather (its 384-B records: 106.5 -> 56.4 GB fetched per launch,
-    round 5), row order for the others (config E: 35.8 vs 36.3, 36.0 vs 36.2, 35.13 vs 35.29 ms on three
-    boxes; C 0.99 vs 1.01 ms)."""
+    locality: the chunk visiting order (_plan_locality: "morton" / True, "deal", "row" / False); None
+    (default): "deal" for the neo-Hookean gather (62.1 vs 63.2 ms Morton on E-neo), "row" for the others
+    (config E: 35.8 vs 36.3, 36.0 vs 36.2, 35.13 vs 35.29 ms Morton on three boxes; C 0.99 vs 1.01 ms;
+    DESIGN.md §4)."""
     if deterministic and owner:
         raise ValueError("deterministic assembly runs the LDS-atomic gather: owner=True (block-owner plan) "
                          "cannot be combined with deterministic=True")
     neo = kind == _lib.FA_NEO_HOOKEAN
     if locality is None:
-        locality = neo
+        locality = "deal" if neo else "row"
     if neo and not (slots and order == "positional"):
         raise ValueError("the neo-Hookean gather needs positional plans (slots=True, order='positional')")
     plans = V.__dict__.setdefault("_plans", {})
@@ -812,8 +824,8 @@ class SplitGather:
             self.plans.append(plan)
             self._keep.append(rs)
             if r1 > r0:
-                self._keep.append(_plan_locality(V, self.fm, self.adj, plan, self.sh,
-                                                 locality=a.kind == _lib.FA_NEO_HOOKEAN))  # (gather_plan's default)
+                self._keep.append(_plan_locality(V, self.fm, self.adj, plan, self.sh,  # (gather_plan's default)
+                                                 locality="deal" if a.kind == _lib.FA_NEO_HOOKEAN else "row"))
         if self.slots is not None:
             # one slot map for all rows (fa_plan_slots writes every row), then each plan's order
             live = [i for i, (r0, r1) in enumerate(ranges) if r1 > r0]

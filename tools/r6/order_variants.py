@@ -34,10 +34,11 @@ def timed(fn, reps, warm=2):
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 203
     variants = sys.argv[2].split(",") if len(sys.argv) > 2 else ["morton", "row", "deal16", "deal1", "morton"]
+    cfg = bench.CONFIGS[sys.argv[3] if len(sys.argv) > 3 else "E"]
     dev = torch.device("cuda", 0)
-    m, V, a, bcs = bench.build_problem(n, dev)
+    m, V, a, bcs = bench.build_problem(n, dev, cfg=cfg)
     A = fem.create_matrix(a)
-    plan = fem.gather_plan(V, A, 0, a.kind)
+    plan = fem.gather_plan(V, A, 0, a.kind, locality=True)
     morton = plan.corder
     nch = int(plan.nchunks)
     ref = None
