@@ -137,6 +137,24 @@ V = {
               "      constexpr int OOB = 0x40000000, NTS = 1;  // nt\n      // one descriptor over the chunk's nv values")],
     "nts3": [("      constexpr int OOB = 0x40000000, NTS = 2;  // nt\n      // one descriptor over the chunk's nv values",
               "      constexpr int OOB = 0x40000000, NTS = 3;  // nt\n      // one descriptor over the chunk's nv values")],
+    # (round 6) every drain's store cache policy (k_gather_lin's inline drain and xchg_drain): plain / sc0 sc1
+    "xnts0": [("constexpr int OOB = 0x40000000, NTS = 2;  // nt\n", "constexpr int OOB = 0x40000000, NTS = 0;  // nt\n")],
+    "xnts3": [("constexpr int OOB = 0x40000000, NTS = 2;  // nt\n", "constexpr int OOB = 0x40000000, NTS = 3;  // nt\n")],
+    # (round 6) k_gather_lin / k_gather_neo: an XCD whose eighth of the visiting sequence is used up takes
+    # the next chunks of the other XCDs' eighths (work stealing at the tail, the eighths stay contiguous)
+    "steal": [(
+        "  auto chunk_of = [&](unsigned int j) -> int32_t {\n"
+        "    return (int32_t)(j < uper ? min((unsigned)xc * uper + j, unc) : unc);\n  };",
+        "  auto chunk_of = [&](unsigned int j) -> int32_t {\n"
+        "    if (j < uper) return (int32_t)min((unsigned)xc * uper + j, unc);\n"
+        "    for (int s = 1; s < 8; ++s) {\n"
+        "      const int v = (xc + s) & 7;\n"
+        "      unsigned int* const vc = reinterpret_cast<unsigned int*>(P.ctr) + 32 * v;\n"
+        "      if (__hip_atomic_load(vc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= uper) continue;\n"
+        "      const unsigned int r = atomicInc(vc, 0xFFFFFFFFu);\n"
+        "      if (r < uper) return (int32_t)min((unsigned)v * uper + r, unc);\n"
+        "    }\n"
+        "    return (int32_t)unc;\n  };")],
     # P1 simplices through the records kernel + k_gather_lin (no fused records)
     "nofuse": [("constexpr int FA_LIN_FUSE = 1;", "constexpr int FA_LIN_FUSE = 0;")],
     # k_gather_neo in 2-wave workgroups (128 items, chunks of <= 64 entries, 23 KB accumulator): 4
