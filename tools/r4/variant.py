@@ -141,20 +141,28 @@ V = {
     "xnts0": [("constexpr int OOB = 0x40000000, NTS = 2;  // nt\n", "constexpr int OOB = 0x40000000, NTS = 0;  // nt\n")],
     "xnts3": [("constexpr int OOB = 0x40000000, NTS = 2;  // nt\n", "constexpr int OOB = 0x40000000, NTS = 3;  // nt\n")],
     # (round 6) k_gather_lin / k_gather_neo: an XCD whose eighth of the visiting sequence is used up takes
-    # the next chunks of the other XCDs' eighths (work stealing at the tail, the eighths stay contiguous)
+    # the next chunks of the other XCDs' eighths (work stealing at the tail, the eighths stay contiguous;
+    # an eighth's length clipped at nchunks so an empty id is final). Measured E -0.5 %, not shipped:
+    # DESIGN.md §4 (suite failures with it in the product library, unexplained)
     "steal": [(
         "  auto chunk_of = [&](unsigned int j) -> int32_t {\n"
         "    return (int32_t)(j < uper ? min((unsigned)xc * uper + j, unc) : unc);\n  };",
+        "  auto len_of = [&](int x) -> unsigned int {\n"
+        "    const unsigned int b = (unsigned)x * uper;\n"
+        "    return b >= unc ? 0u : min(uper, unc - b);\n  };\n"
         "  auto chunk_of = [&](unsigned int j) -> int32_t {\n"
-        "    if (j < uper) return (int32_t)min((unsigned)xc * uper + j, unc);\n"
+        "    if (j < len_of(xc)) return (int32_t)((unsigned)xc * uper + j);\n"
         "    for (int s = 1; s < 8; ++s) {\n"
         "      const int v = (xc + s) & 7;\n"
+        "      const unsigned int lv = len_of(v);\n"
         "      unsigned int* const vc = reinterpret_cast<unsigned int*>(P.ctr) + 32 * v;\n"
-        "      if (__hip_atomic_load(vc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= uper) continue;\n"
+        "      if (__hip_atomic_load(vc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= lv) continue;\n"
         "      const unsigned int r = atomicInc(vc, 0xFFFFFFFFu);\n"
-        "      if (r < uper) return (int32_t)min((unsigned)v * uper + r, unc);\n"
+        "      if (r < lv) return (int32_t)((unsigned)v * uper + r);\n"
         "    }\n"
         "    return (int32_t)unc;\n  };")],
+    # the source as it is (A/B base of an edited product library)
+    "base": [],
     # P1 simplices through the records kernel + k_gather_lin (no fused records)
     "nofuse": [("constexpr int FA_LIN_FUSE = 1;", "constexpr int FA_LIN_FUSE = 0;")],
     # k_gather_neo in 2-wave workgroups (128 items, chunks of <= 64 entries, 23 KB accumulator): 4
