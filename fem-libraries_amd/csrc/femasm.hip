@@ -179,11 +179,16 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
   if (is_simplex(ct)) {
     simplex_ahat(T, ah, amax);
     h.insert(h.end(), ah.begin(), ah.end());
+  } else if (ct == FA_QUADRILATERAL) {
+    // affine quadrilaterals (parallelograms) share the simplex form: one Jacobian per cell, so
+    // k_gather_lin reads the same packed table (round 6); the Gauss rule integrates it exactly
+    double am = 0.0;
+    simplex_ahat(T, ah, am);
   }
   std::vector<uint64_t> pk;
   double pk_scale = 0.0, pk_amax = 0.0;
   size_t off_pk = 0;
-  if (is_simplex(ct) && pack_ahat(T.nn, T.td, ah, pk, pk_scale, pk_amax)) {
+  if ((is_simplex(ct) || ct == FA_QUADRILATERAL) && pack_ahat(T.nn, T.td, ah, pk, pk_scale, pk_amax)) {
     off_pk = h.size();
     for (uint64_t q : pk) {
       double d;
@@ -248,8 +253,8 @@ extern "C" int fa_element_info(int32_t cell_type, int32_t degree, int32_t qdeg, 
 }
 
 // Host only (no device call): whether the element's reference tensor packs into the integer table the
-// P2 / P3 simplex gather reads (k_gather_lin), and its denominator D (Ahat = N / D); 0 = not packed
-// (the kernel then falls back to the generic gather).
+// table gather reads (k_gather_lin: P2 / P3 simplices, affine quadrilaterals), and its denominator D
+// (Ahat = N / D); 0 = not packed (the kernel then falls back to the generic gather).
 extern "C" int fa_element_table_info(int32_t cell_type, int32_t degree, int32_t qdeg, int32_t* packed_denom,
                                      double* amax) {
   if (!supported(cell_type, degree)) return fail(FA_E_UNSUPPORTED, "unsupported element: cell %d degree %d", cell_type, degree);
@@ -257,7 +262,7 @@ extern "C" int fa_element_table_info(int32_t cell_type, int32_t degree, int32_t 
   if (qd > 12) return fail(FA_E_UNSUPPORTED, "quadrature degree %d > 12", qd);
   int D = 0;
   double am = 0.0;
-  if (is_simplex(cell_type)) {
+  if (is_simplex(cell_type) || cell_type == FA_QUADRILATERAL) {
     ElementTables T;
     if (!make_tables(cell_type, degree, qd, T)) return fail(FA_E_UNSUPPORTED, "element tables failed");
     std::vector<double> ah;
@@ -1649,7 +1654,8 @@ __global__ __launch_bounds__(256) void k_cell_records_staged(MeshView M, FormVie
     cell_record<GD, NN, NV, NQ, MAT>(M, F, tab, cc, r);
     uint32_t m = 0u;
     if (bcmask && valid) m = cell_bcmask<GD, NN>(M, bc, c);
-    if constexpr (MAT == MAT_LINU && NN * GD <= 32)  // the mask also rides in the sign word (rec_sign)
+    // the mask also rides in the sign word (rec_sign; affine tensor cells too: k_gather_lin reads them)
+    if constexpr ((MAT == MAT_LINU || MAT == MAT_AFFT) && NN * GD <= 32)
       r[GD * GD] = __longlong_as_double(__double_as_longlong(r[GD * GD]) | (long long)m);
 #pragma unroll
     for (int k = 0; k < R::SIZE; ++k) sb[lane * R::SIZE + k] = r[k];
@@ -4349,14 +4355,22 @@ constexpr int FA_P2TET_NSPLIT = 2;  // measured best with the reference-tensor b
 // affine tensor cells: column nodes per item = NN / NSPLIT
 constexpr int FA_Q2HEX_NSPLIT = 9;
 constexpr int FA_Q3HEX_NSPLIT = 32;
-constexpr int FA_Q2QUAD_NSPLIT = 3;
+// Q2 quadrilaterals: whole entries (9 blocks per item) since round 6, when affine ones moved to
+// k_gather_lin: its positional plans fill 16-lane quarters with whole entries (16 % NSPLIT == 0), which
+// 3 does not divide (the generic gather had used 3 with searched slots)
+constexpr int FA_Q2QUAD_NSPLIT = 1;
 constexpr int FA_P1TET_NSPLIT = 1;  // P1 tetrahedra: whole entries (4 blocks per item); config C 1.86 vs 1.97 ms (2), 2.25 (4)
 // k_gather_lin's workgroup size (one item per thread, chunks of up to NT / NSPLIT entries): P1
 // tetrahedra have 4-block items, so their chunks are short on work per barrier at 256 items
 constexpr int FA_P1TET_NT = 256;  // 512 measured 1.72 vs 1.68 ms on config C
 constexpr int FA_P2TET_NT = 256;
+// affine Q2 quadrilaterals (whole 9-block entries): the 1023-block cap of a chunk binds at ~144
+// entries, so 256-item workgroups ran half empty; 128 items measured config B 0.534 vs 0.612 ms
+// (192: 0.572; 128 items with a 767 / 511-block accumulator for more resident workgroups: 0.574 /
+// 0.640; 64 items: 0.59-0.66; profiles/r6/q2quad_nt_ab.txt)
+constexpr int FA_Q2QUAD_NT = 128;
 __host__ __device__ constexpr int lin_threads(int gd, int nn) {
-  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : 256;
+  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : gd == 2 && nn == 9 ? FA_Q2QUAD_NT : 256;
 }
 static int lin_simplex_nsplit(int ct, int p, int nq, bool affine = false) {
   // affine hexahedra (MAT_AFFT): Q1 / Q2 / Q3 with their default rules
@@ -4433,7 +4447,7 @@ extern "C" int fa_plan_order(const fa_mesh* mesh, const fa_adjacency* adj, const
   else if (mesh->nn == 27 && ns == FA_Q2HEX_NSPLIT) ORD(27, FA_Q2HEX_NSPLIT);
   else if (mesh->nn == 64 && ns == FA_Q3HEX_NSPLIT) ORD(64, FA_Q3HEX_NSPLIT);
   else if (mesh->nn == 4 && ns == 1) ORD(4, 1);
-  else if (mesh->nn == 9 && ns == FA_Q2QUAD_NSPLIT) ORD(9, FA_Q2QUAD_NSPLIT);
+  else if (mesh->nn == 9 && ns == 1) ORD(9, 1);
   else if (mesh->nn == 16 && ns == 4) ORD(16, 4);
   else ok = false;
 #undef ORD
@@ -4624,6 +4638,18 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
     if (rc) return rc;
     const int ns = lin_simplex_nsplit(mesh->cell_type, mesh->degree, T.nq);
     if (ns > 0) {
+      maxadj = std::min(maxadj, lin_threads(mesh->gdim, mesh->nn) / ns);
+      return plan_gather(mesh, adj, A, row_start, plan, stream, lin_maxb(mesh->gdim, mesh->nn), maxadj);
+    }
+  }
+  // quadrilaterals: k_gather_lin's caps too (affine cells of a packed table run it, round 6; the
+  // generic gather of other quadrilaterals reads the same plan)
+  if (mesh->cell_type == FA_QUADRILATERAL) {
+    DevTables T;
+    int rc = get_tables(mesh->cell_type, mesh->degree, -1, &T);
+    if (rc) return rc;
+    const int ns = lin_simplex_nsplit(mesh->cell_type, mesh->degree, T.nq, true);
+    if (ns > 0 && T.pk) {
       maxadj = std::min(maxadj, lin_threads(mesh->gdim, mesh->nn) / ns);
       return plan_gather(mesh, adj, A, row_start, plan, stream, lin_maxb(mesh->gdim, mesh->nn), maxadj);
     }
@@ -5348,8 +5374,11 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   }
   P.rec = rec;
   P.bcmask = mask;
-  if constexpr (MAT == MAT_LINU && R::SIMP && NN % NSPLIT == 0 && NN * GD <= 32 && NN < 64) {
-    // the store-decoupled gather (k_gather_lin): positional plans of <= 256 items per chunk
+  // the store-decoupled gather (k_gather_lin): positional plans of <= 256 items per chunk; affine
+  // simplices, and (round 6) affine quadrilaterals, whose uniform-nu records (s Ji, sign and bc bits)
+  // are the simplices' and whose reference tensor packs the same way (get_tables)
+  if constexpr ((MAT == MAT_LINU || (MAT == MAT_AFFT && GD == 2)) && R::SIMP && NN % NSPLIT == 0 && NN * GD <= 32 &&
+                NN < 64) {
     constexpr int LNT = lin_threads(GD, NN);
     if (P.nchunks > 0 && W.mode != GatherStage::PREP && !P.cw && P.eadj && P.slots && (NN == GD + 1 || P.pk) &&
         P.slot_order == NSPLIT && !P.corder && P.plan_maxadj * NSPLIT <= LNT && P.plan_maxadj >= 0) {

@@ -161,6 +161,18 @@ V = {
         "      if (r < lv) return (int32_t)((unsigned)v * uper + r);\n"
         "    }\n"
         "    return (int32_t)unc;\n  };")],
+    # (round 6) affine Q2 quadrilaterals through k_gather_lin: workgroups of 128 / 192 items (chunks of at
+    # most that many whole entries; at 256 the 1023-block cap binds first, ~144 entries). Patterns of the
+    # source before FA_Q2QUAD_NT (128, adopted): kept as the record of profiles/r6/q2quad_nt_ab.txt
+    "q2quad_nt128": [("  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : 256;",
+                      "  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : gd == 2 && nn == 9 ? 128 : 256;")],
+    "q2quad_nt192": [("  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : 256;",
+                      "  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : gd == 2 && nn == 9 ? 192 : 256;")],
+    # ... and smaller accumulators (more resident workgroups): items per workgroup / blocks per chunk
+    "q2quad_nt128_b767": [('  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : 256;', '  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : gd == 2 && nn == 9 ? 128 : 256;'), ('  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gather_maxb(false, gd * gd);', '  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gd == 2 && nn == 9 ? 767 : gather_maxb(false, gd * gd);')],
+    "q2quad_nt128_b511": [('  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : 256;', '  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : gd == 2 && nn == 9 ? 128 : 256;'), ('  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gather_maxb(false, gd * gd);', '  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gd == 2 && nn == 9 ? 511 : gather_maxb(false, gd * gd);')],
+    "q2quad_nt64_b511": [('  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : 256;', '  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : gd == 2 && nn == 9 ? 64 : 256;'), ('  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gather_maxb(false, gd * gd);', '  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gd == 2 && nn == 9 ? 511 : gather_maxb(false, gd * gd);')],
+    "q2quad_nt64_b383": [('  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : 256;', '  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : gd == 2 && nn == 9 ? 64 : 256;'), ('  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gather_maxb(false, gd * gd);', '  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gd == 2 && nn == 9 ? 383 : gather_maxb(false, gd * gd);')],
     # the source as it is (A/B base of an edited product library)
     "base": [],
     # P1 simplices through the records kernel + k_gather_lin (no fused records)

@@ -4,5 +4,5 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-CFGS="${CFGS:-E:203 C:119 Eneo:203 D:58 Dmfma:58}" bash tools/gpu_traffic.sh > gpurun_out/traffic_rel1.txt 2>&1 || { tail -5 gpurun_out/traffic_rel1.txt; exit 1; }
+CFGS="${CFGS:-E:203 C:119 Eneo:203 D:58 Dmfma:58 B:1000}" bash tools/gpu_traffic.sh > gpurun_out/traffic_rel1.txt 2>&1 || { tail -5 gpurun_out/traffic_rel1.txt; exit 1; }
 tail -3 gpurun_out/traffic_rel1.txt | cut -c1-300
