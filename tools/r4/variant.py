@@ -173,6 +173,10 @@ V = {
     "q2quad_nt128_b511": [('  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : 256;', '  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : gd == 2 && nn == 9 ? 128 : 256;'), ('  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gather_maxb(false, gd * gd);', '  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gd == 2 && nn == 9 ? 511 : gather_maxb(false, gd * gd);')],
     "q2quad_nt64_b511": [('  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : 256;', '  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : gd == 2 && nn == 9 ? 64 : 256;'), ('  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gather_maxb(false, gd * gd);', '  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gd == 2 && nn == 9 ? 511 : gather_maxb(false, gd * gd);')],
     "q2quad_nt64_b383": [('  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : 256;', '  return gd == 3 && nn == 4 ? FA_P1TET_NT : gd == 3 && nn == 10 ? FA_P2TET_NT : gd == 2 && nn == 9 ? 64 : 256;'), ('  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gather_maxb(false, gd * gd);', '  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gd == 2 && nn == 9 ? 383 : gather_maxb(false, gd * gd);')],
+    # (round 6) config E: a larger k_gather_lin accumulator for P2 tets (455 blocks = 32 KB; 4 workgroups
+    # of ~40 KB still fit a CU's 160 KB): chunks fill more of their 128 entries
+    "p2tet_b500": [('  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gather_maxb(false, gd * gd);', '  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gd == 3 && nn == 10 ? 500 : gather_maxb(false, gd * gd);'), ('  if (P.plan_maxb > gather_maxb(false, GD * GD))\n    return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, this form\'s kernel %d: plan with fa_plan_gather_form",\n                P.plan_maxb, gather_maxb(false, GD * GD));', '  if (P.plan_maxb > std::max(gather_maxb(false, GD * GD), lin_maxb(GD, NN)))\n    return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, this form\'s kernel %d: plan with fa_plan_gather_form",\n                P.plan_maxb, gather_maxb(false, GD * GD));')],
+    "p2tet_b540": [('  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gather_maxb(false, gd * gd);', '  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gd == 3 && nn == 10 ? 540 : gather_maxb(false, gd * gd);'), ('  if (P.plan_maxb > gather_maxb(false, GD * GD))\n    return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, this form\'s kernel %d: plan with fa_plan_gather_form",\n                P.plan_maxb, gather_maxb(false, GD * GD));', '  if (P.plan_maxb > std::max(gather_maxb(false, GD * GD), lin_maxb(GD, NN)))\n    return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, this form\'s kernel %d: plan with fa_plan_gather_form",\n                P.plan_maxb, gather_maxb(false, GD * GD));')],
     # the source as it is (A/B base of an edited product library)
     "base": [],
     # P1 simplices through the records kernel + k_gather_lin (no fused records)
