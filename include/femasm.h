@@ -74,9 +74,9 @@ extern "C" {
  * order, then converts it back with one rounding: the values are identical run to run. Every cell
  * adding into block (a, b) holds node a, so a row's values are within ~2^-50 per summand of its own
  * cells' scale, at any stiffness contrast between rows (the per-row 1e-12 bar is tested at contrasts
- * 1e2 .. 1e8, tests/test_gpu_deterministic.py; rounds 4-5 had one scale per row chunk). For affine-simplex
- * linear elasticity with one Poisson ratio (the k_gather_lin kernels) and a positional plan; other
- * forms return FA_E_UNSUPPORTED. (The reference's MFEM integrator is likewise order-fixed: it runs
+ * 1e2 .. 1e8, tests/test_gpu_deterministic.py; rounds 4-5 had one scale per row chunk). For linear
+ * elasticity with one Poisson ratio on affine simplices and (round 6) affine Q1 / Q2 quadrilaterals (the
+ * k_gather_lin kernels) with a positional plan; other forms return FA_E_UNSUPPORTED. (The reference's MFEM integrator is likewise order-fixed: it runs
  * one thread, MFEM/mechanic2d/asym_elasto_damage_model.cc:27.) */
 
 typedef struct {
@@ -163,10 +163,11 @@ int fa_version(void);
 /* Element metadata: nodes per cell and quadrature points for (cell_type, degree, qdeg). */
 int fa_element_info(int32_t cell_type, int32_t degree, int32_t qdeg, int32_t* nn, int32_t* nq);
 
-/* Host-only (no device call): whether a simplex element's reference tensor Ahat (default rule for
- * qdeg < 0) is exactly N / D with small integers, i.e. packs into the integer table the P2 / P3 simplex
- * gather reads; *packed_denom = D, or 0 when it does not pack (that element then assembles through the
- * generic gather) or for tensor cells. *amax = max |Ahat| (simplices). Either pointer may be NULL. */
+/* Host-only (no device call): whether an element's reference tensor Ahat (default rule for qdeg < 0)
+ * is exactly N / D with small integers, i.e. packs into the integer table the store-decoupled gather
+ * reads (simplices; affine quadrilaterals since round 6, e.g. Q2: D = 180); *packed_denom = D, or 0
+ * when it does not pack (that element then assembles through the generic gather) or for hexahedra.
+ * *amax = max |Ahat|. Either pointer may be NULL. */
 int fa_element_table_info(int32_t cell_type, int32_t degree, int32_t qdeg, int32_t* packed_denom, double* amax);
 
 /* Node -> cell adjacency (transpose of the dofmap): ptr [nnodes+1], idx [ncells*nn]. */
