@@ -177,6 +177,10 @@ V = {
     # of ~40 KB still fit a CU's 160 KB): chunks fill more of their 128 entries
     "p2tet_b500": [('  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gather_maxb(false, gd * gd);', '  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gd == 3 && nn == 10 ? 500 : gather_maxb(false, gd * gd);'), ('  if (P.plan_maxb > gather_maxb(false, GD * GD))\n    return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, this form\'s kernel %d: plan with fa_plan_gather_form",\n                P.plan_maxb, gather_maxb(false, GD * GD));', '  if (P.plan_maxb > std::max(gather_maxb(false, GD * GD), lin_maxb(GD, NN)))\n    return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, this form\'s kernel %d: plan with fa_plan_gather_form",\n                P.plan_maxb, gather_maxb(false, GD * GD));')],
     "p2tet_b540": [('  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gather_maxb(false, gd * gd);', '  return nn == gd + 1 ? kLinLdsP1 / (8 * gd * gd) : gd == 3 && nn == 10 ? 540 : gather_maxb(false, gd * gd);'), ('  if (P.plan_maxb > gather_maxb(false, GD * GD))\n    return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, this form\'s kernel %d: plan with fa_plan_gather_form",\n                P.plan_maxb, gather_maxb(false, GD * GD));', '  if (P.plan_maxb > std::max(gather_maxb(false, GD * GD), lin_maxb(GD, NN)))\n    return fail(FA_E_ARG, "gather plan chunks hold up to %d blocks, this form\'s kernel %d: plan with fa_plan_gather_form",\n                P.plan_maxb, gather_maxb(false, GD * GD));')],
+    # (round 6) config C: k_gather_lin P1-tet workgroups of 128 items (the Q2-quad lesson), accumulator 16 / 8 KB
+    "p1tet_nt128": [('constexpr int FA_P1TET_NT = 256;', 'constexpr int FA_P1TET_NT = 128;')],
+    "p1tet_nt128_lds8k": [('constexpr int FA_P1TET_NT = 256;', 'constexpr int FA_P1TET_NT = 128;'), ('constexpr int kLinLdsP1 = 16384;', 'constexpr int kLinLdsP1 = 8192;')],
+    "p1tet_lds24k": [('constexpr int kLinLdsP1 = 16384;', 'constexpr int kLinLdsP1 = 24576;')],
     # the source as it is (A/B base of an edited product library)
     "base": [],
     # P1 simplices through the records kernel + k_gather_lin (no fused records)
