@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 6 batch 17: the whole GPU suite three times on the release library (intermittent-failure check)
+# round 6 batch 26: the whole GPU suite three times on the release library (intermittent-failure check)
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
