@@ -28,3 +28,16 @@ def lame(E, nu: float):
     mu = E / (2.0 * (1.0 + nu))
     lmbda = E * nu / ((1.0 + nu) * (1.0 - 2.0 * nu))
     return lmbda, mu
+
+
+def e_from_cell_tags(tags, num_cells: int, seed: int = 6575):
+    """E per cell from the cell tags (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:543-545:
+    ``E_range[phys % 200]`` over ``cell_tag.values()``): a torch float64 tensor [num_cells] on the
+    tags' device. Every cell must carry a tag (the reference indexes the values by cell)."""
+    import torch
+
+    if tags.indices.numel() != num_cells or not bool(
+            (tags.indices.to(torch.int64) == torch.arange(num_cells, device=tags.indices.device)).all()):
+        raise ValueError(f"cell tags cover {tags.indices.numel()} of {num_cells} cells: E needs a tag on every cell")
+    er = torch.tensor(e_range(seed), dtype=torch.float64, device=tags.values.device)
+    return er[tags.values.to(torch.int64) % 200]

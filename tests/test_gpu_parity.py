@@ -181,6 +181,29 @@ def test_reference_square_msh(oracle, dev):
     assert_rows_close(A.data.cpu().numpy(), gold["data"], gold["indptr"], RTOL)
 
 
+def test_reference_square_through_xdmf(oracle, dev, tmp_path):
+    """The reference driver's input path (FEniCSx/mechanic2d/asym_elasto_damage_model.cc:155-162,
+    :543-545): mesh and cell tags read from an XDMF file (the square.msh mesh written with
+    femasm.io), E from the tags, assembled on the GPU: the same matrix as the golden square.msh case."""
+    from femasm import fem, io, materials, mesh
+
+    g = mesh.read_gmsh(os.path.join(GOLDEN, "square.msh"), gdim=2)
+    tags = io.MeshTags(2, torch.arange(g.num_cells, dtype=torch.int32), g.cell_tags, "square_cells")
+    path = str(tmp_path / "square.xdmf")
+    with io.XDMFFile(path, "w") as f:
+        f.write_mesh(g, "square")
+        f.write_meshtags(tags, g)
+    with io.XDMFFile(path) as f:
+        m = f.read_mesh("square", device=dev)
+        t = f.read_meshtags(m, "square_cells")
+    V = fem.functionspace(m, ("Lagrange", 1, (2,)))
+    a = fem.LinearElasticity(V, E=materials.e_from_cell_tags(t, m.num_cells), nu=0.3, quadrature_degree=1)
+    A = fem.assemble_matrix(a)
+    gold = np.load(os.path.join(GOLDEN, "square_p1_elasticity.npz"))
+    np.testing.assert_array_equal(A.indices.cpu().numpy(), gold["indices"])
+    assert_rows_close(A.data.cpu().numpy(), gold["data"], gold["indptr"], RTOL)
+
+
 @pytest.mark.parametrize("method", ["gather", "scatter"])
 def test_damage_law_matches_oracle(oracle, dev, method):
     """Reference mechanic2d J with damage (MFEM hand tangent restated), random u and d."""
