@@ -475,7 +475,12 @@ def main():
         import torch.distributed as dist
 
         if backend == "nccl":
-            # RCCL over xGMI; a bounded timeout so that a stuck exchange ends in an error, not a hang
+            # RCCL over xGMI; a bounded timeout so that a stuck exchange ends in an error, not a hang.
+            # Blocking waits without the watchdog's abort: a timed-out or failed transfer of the exchange
+            # leg then raises in this process (caught below: the ghost leg's line stands) instead of the
+            # watchdog tearing the process down before rank 0 prints (a caller's setting is kept)
+            os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
             import datetime
 
             dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=180))
