@@ -179,16 +179,17 @@ static int get_tables(int ct, int p, int qdeg, DevTables* out) {
   if (is_simplex(ct)) {
     simplex_ahat(T, ah, amax);
     h.insert(h.end(), ah.begin(), ah.end());
-  } else if (ct == FA_QUADRILATERAL) {
-    // affine quadrilaterals (parallelograms) share the simplex form: one Jacobian per cell, so
-    // k_gather_lin reads the same packed table (round 6); the Gauss rule integrates it exactly
+  } else if (ct == FA_QUADRILATERAL || (ct == FA_HEXAHEDRON && p == 1)) {
+    // affine quadrilaterals (parallelograms) and Q1 parallelepipeds share the simplex form: one
+    // Jacobian per cell, so k_gather_lin reads the same packed table (round 6); the Gauss rule
+    // integrates it exactly (Q2 / Q3 hexahedra have more dofs than a record's 32 bc bits)
     double am = 0.0;
     simplex_ahat(T, ah, am);
   }
   std::vector<uint64_t> pk;
   double pk_scale = 0.0, pk_amax = 0.0;
   size_t off_pk = 0;
-  if ((is_simplex(ct) || ct == FA_QUADRILATERAL) && pack_ahat(T.nn, T.td, ah, pk, pk_scale, pk_amax)) {
+  if (!ah.empty() && pack_ahat(T.nn, T.td, ah, pk, pk_scale, pk_amax)) {
     off_pk = h.size();
     for (uint64_t q : pk) {
       double d;
@@ -262,7 +263,7 @@ extern "C" int fa_element_table_info(int32_t cell_type, int32_t degree, int32_t 
   if (qd > 12) return fail(FA_E_UNSUPPORTED, "quadrature degree %d > 12", qd);
   int D = 0;
   double am = 0.0;
-  if (is_simplex(cell_type) || cell_type == FA_QUADRILATERAL) {
+  if (is_simplex(cell_type) || cell_type == FA_QUADRILATERAL || (cell_type == FA_HEXAHEDRON && degree == 1)) {
     ElementTables T;
     if (!make_tables(cell_type, degree, qd, T)) return fail(FA_E_UNSUPPORTED, "element tables failed");
     std::vector<double> ah;
@@ -4642,9 +4643,9 @@ extern "C" int fa_plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, cons
       return plan_gather(mesh, adj, A, row_start, plan, stream, lin_maxb(mesh->gdim, mesh->nn), maxadj);
     }
   }
-  // quadrilaterals: k_gather_lin's caps too (affine cells of a packed table run it, round 6; the
-  // generic gather of other quadrilaterals reads the same plan)
-  if (mesh->cell_type == FA_QUADRILATERAL) {
+  // quadrilaterals and Q1 hexahedra: k_gather_lin's caps too (affine cells of a packed table run it,
+  // round 6; the generic gather of the others reads the same plan)
+  if (mesh->cell_type == FA_QUADRILATERAL || (mesh->cell_type == FA_HEXAHEDRON && mesh->degree == 1)) {
     DevTables T;
     int rc = get_tables(mesh->cell_type, mesh->degree, -1, &T);
     if (rc) return rc;
@@ -5375,10 +5376,9 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
   P.rec = rec;
   P.bcmask = mask;
   // the store-decoupled gather (k_gather_lin): positional plans of <= 256 items per chunk; affine
-  // simplices, and (round 6) affine quadrilaterals, whose uniform-nu records (s Ji, sign and bc bits)
-  // are the simplices' and whose reference tensor packs the same way (get_tables)
-  if constexpr ((MAT == MAT_LINU || (MAT == MAT_AFFT && GD == 2)) && R::SIMP && NN % NSPLIT == 0 && NN * GD <= 32 &&
-                NN < 64) {
+  // simplices, and (round 6) affine quadrilaterals / Q1 hexahedra, whose uniform-nu records (s Ji, sign
+  // and bc bits) are the simplices' and whose reference tensor packs the same way (get_tables)
+  if constexpr ((MAT == MAT_LINU || MAT == MAT_AFFT) && R::SIMP && NN % NSPLIT == 0 && NN * GD <= 32 && NN < 64) {
     constexpr int LNT = lin_threads(GD, NN);
     if (P.nchunks > 0 && W.mode != GatherStage::PREP && !P.cw && P.eadj && P.slots && (NN == GD + 1 || P.pk) &&
         P.slot_order == NSPLIT && !P.corder && P.plan_maxadj * NSPLIT <= LNT && P.plan_maxadj >= 0) {

@@ -742,8 +742,8 @@ def assemble_matrix(a, bcs=None, diagonal: float = 1.0, A: MatrixCSR | None = No
     diagonal entries are set to `diagonal`. method: "gather" (row-gather, default) or
     "scatter" (element scatter with FP64 atomics; zeroes A first like MatZeroEntries).
     deterministic: bit-identical values run to run (FA_DETERMINISTIC: exact 64-bit fixed-point
-    sums in the gather; linear elasticity with one Poisson ratio on affine simplices and affine Q1 / Q2
-    quadrilaterals).
+    sums in the gather; linear elasticity with one Poisson ratio on affine simplices, affine Q1 / Q2
+    quadrilaterals and Q1 hexahedra).
     plan: gather_plan options (owner, slots, order, locality). check: synchronise and raise if a
     kernel found a pattern entry missing (FA_CHECK_ERRORS).
     """

@@ -75,7 +75,8 @@ extern "C" {
  * adding into block (a, b) holds node a, so a row's values are within ~2^-50 per summand of its own
  * cells' scale, at any stiffness contrast between rows (the per-row 1e-12 bar is tested at contrasts
  * 1e2 .. 1e8, tests/test_gpu_deterministic.py; rounds 4-5 had one scale per row chunk). For linear
- * elasticity with one Poisson ratio on affine simplices and (round 6) affine Q1 / Q2 quadrilaterals (the
+ * elasticity with one Poisson ratio on affine simplices and (round 6) affine Q1 / Q2 quadrilaterals and Q1
+ * hexahedra (the
  * k_gather_lin kernels) with a positional plan; other forms return FA_E_UNSUPPORTED. (The reference's MFEM integrator is likewise order-fixed: it runs
  * one thread, MFEM/mechanic2d/asym_elasto_damage_model.cc:27.) */
 
@@ -165,8 +166,9 @@ int fa_element_info(int32_t cell_type, int32_t degree, int32_t qdeg, int32_t* nn
 
 /* Host-only (no device call): whether an element's reference tensor Ahat (default rule for qdeg < 0)
  * is exactly N / D with small integers, i.e. packs into the integer table the store-decoupled gather
- * reads (simplices; affine quadrilaterals since round 6, e.g. Q2: D = 180); *packed_denom = D, or 0
- * when it does not pack (that element then assembles through the generic gather) or for hexahedra.
+ * reads (simplices; affine quadrilaterals and Q1 hexahedra since round 6, e.g. Q2 quads: D = 180);
+ * *packed_denom = D, or 0 when it does not pack (that element then assembles through the generic gather)
+ * or for Q2 / Q3 hexahedra.
  * *amax = max |Ahat|. Either pointer may be NULL. */
 int fa_element_table_info(int32_t cell_type, int32_t degree, int32_t qdeg, int32_t* packed_denom, double* amax);
 

@@ -61,11 +61,12 @@ def test_version_and_element_info():
     assert b"unsupported" in L.fa_last_error()
 
 
-@pytest.mark.parametrize("ct,p,denom", [(3, 1, 2), (3, 2, 6), (-4, 1, 6), (-4, 2, 30), (4, 1, 12), (4, 2, 180)])
+@pytest.mark.parametrize("ct,p,denom", [(3, 1, 2), (3, 2, 6), (-4, 1, 6), (-4, 2, 30), (4, 1, 12), (4, 2, 180),
+                                         (8, 1, 72)])
 def test_simplex_reference_tensors_pack(ct, p, denom):
-    """The P1/P2 triangle and tetrahedron and the Q1/Q2 quadrilateral default rules give
+    """The P1/P2 triangle and tetrahedron, Q1/Q2 quadrilateral and Q1 hexahedron default rules give
     reference tensors that are exactly N / D (small integers): the packed table the k_gather_lin
-    kernels read (affine quadrilaterals since round 6). A rounding drift past pack_ahat's tolerance
+    kernels read (affine quadrilaterals and Q1 hexahedra since round 6). A rounding drift past pack_ahat's tolerance
     would silently route them to the slower generic gather."""
     from femasm import _lib
 
@@ -76,7 +77,7 @@ def test_simplex_reference_tensors_pack(ct, p, denom):
     assert L.fa_element_table_info(ct, p, -1, ctypes.byref(D), ctypes.byref(amax)) == 0
     assert D.value == denom, (ct, p, D.value)
     assert amax.value > 0.0
-    assert L.fa_element_table_info(8, 2, -1, ctypes.byref(D), None) == 0 and D.value == 0  # hexahedra: none
+    assert L.fa_element_table_info(8, 2, -1, ctypes.byref(D), None) == 0 and D.value == 0  # Q2 hexahedra: none
     assert L.fa_element_table_info(4, 3, -1, ctypes.byref(D), None) == 0 and D.value == 0  # Q3: |N| too large
 
 

@@ -46,9 +46,9 @@ def _oracle(oracle, V, a, bcs):
 
 
 # P1 / P2 tetrahedra (configs C, E) and triangles (config A), each with many chunks; affine Q1 / Q2
-# quadrilaterals (config B's element) run the same gather since round 6
+# quadrilaterals (config B's element) and Q1 hexahedra run the same gather since round 6
 CASES = [(-4, 2, (12, 11, 10)), (-4, 1, (24, 23, 22)), (3, 1, (71, 71)), (3, 2, (40, 37)), (4, 2, (41, 37)),
-         (4, 1, (63, 60))]
+         (4, 1, (63, 60)), (8, 1, (17, 16, 15))]
 
 
 @pytest.mark.parametrize("ct,p,n", CASES)
