@@ -1654,7 +1654,7 @@ __global__ __launch_bounds__(256) void k_cell_records_staged(MeshView M, FormVie
     double r[R::SIZE];
     cell_record<GD, NN, NV, NQ, MAT>(M, F, tab, cc, r);
     uint32_t m = 0u;
-    if (bcmask && valid) m = cell_bcmask<GD, NN>(M, bc, c);
+    if (bcmask && bc && valid) m = cell_bcmask<GD, NN>(M, bc, c);  // (bc NULL: k_rec_bcbits adds the bits)
     // the mask also rides in the sign word (rec_sign; affine tensor cells too: k_gather_lin reads them)
     if constexpr ((MAT == MAT_LINU || MAT == MAT_AFFT) && NN * GD <= 32)
       r[GD * GD] = __longlong_as_double(__double_as_longlong(r[GD * GD]) | (long long)m);
@@ -1675,6 +1675,46 @@ __global__ __launch_bounds__(256) void k_cell_records_staged(MeshView M, FormVie
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (bcmask && valid) bcmask[c] = m;
+  }
+}
+
+// The constrained-dof bits of the uniform-nu records from the constrained nodes' side (round 6): the
+// records kernel then reads no dofmap (40 B per P2 tet of its ~98) and this kernel ORs each constrained
+// node's bits into the records (and the mask array) of the cells around it through the node -> cell
+// adjacency. A wave reads the markers of 64 consecutive nodes (lane = node), then takes its constrained
+// nodes one after the other with a lane per adjacency entry, so an atomic's latency is paid once per
+// constrained node, not once per (node, cell) pair (a thread walking its node's ~24 cells alone: 0.37 ms
+// on config E; per 16 marker bytes and component: 0.66 ms). The same bits as cell_bcmask: bit b * GD + j
+// of cell c for its local node b, component j.
+template <int GD, int NN, int RS>
+__global__ __launch_bounds__(256) void k_rec_bcbits(const int64_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj_idx,
+                                                    const int8_t* __restrict__ bc, int64_t nnodes, double* __restrict__ rec,
+                                                    uint32_t* __restrict__ bcmask) {
+  static_assert(NN * GD <= 32, "bc bits of the record word");
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwv = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t base = wid * 64; base < nnodes; base += nwv * 64) {
+    const int64_t n = base + lane;
+    uint32_t nb = 0u;
+    if (n < nnodes) {
+#pragma unroll
+      for (int j = 0; j < GD; ++j) nb |= (bc[n * GD + j] ? 1u : 0u) << j;
+    }
+    unsigned long long act = __ballot(nb != 0u);
+    while (act) {  // wave-uniform
+      const int l = __ffsll(act) - 1;
+      act &= act - 1;
+      const uint32_t nbl = (uint32_t)__shfl((int)nb, l);
+      const int64_t e0 = adj_ptr[base + l], e1 = adj_ptr[base + l + 1];
+      for (int64_t e = e0 + lane; e < e1; e += 64) {
+        const int64_t p = adj_idx[e];
+        const int64_t c = p / NN;
+        const uint32_t bits = nbl << ((int)(p % NN) * GD);
+        atomicOr(reinterpret_cast<unsigned long long*>(rec + c * RS + GD * GD), (unsigned long long)bits);
+        if (bcmask) atomicOr(bcmask + c, bits);
+      }
+    }
   }
 }
 
@@ -5368,10 +5408,21 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     mask = bc ? reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.work) + rec_bytes) : nullptr;
   }
   if (nc > 0 && W.mode != GatherStage::ROWS) {
+    // uniform-nu records of <= 32 dofs: their bc bits from the constrained nodes (k_rec_bcbits), so the
+    // records kernel reads no dofmap (config E: records 1.88 -> ~1.5 ms)
+    constexpr bool NODE_BITS = (MAT == MAT_LINU || MAT == MAT_AFFT) && NN * GD <= 32 && R::SIZE <= 16;
+    const bool node_bits = NODE_BITS && bc && P.adj_ptr && P.adj_idx;
     if constexpr (R::SIZE <= 16)  // small records: stored through LDS as contiguous runs
-      k_cell_records_staged<GD, NN, NV, NQ, MAT><<<grid_for(nc), 256, 0, s>>>(P.M, P.F, P.tab, bc, rec, mask);
+      k_cell_records_staged<GD, NN, NV, NQ, MAT><<<grid_for(nc), 256, 0, s>>>(P.M, P.F, P.tab, node_bits ? nullptr : bc,
+                                                                             rec, mask);
     else k_cell_records<GD, NN, NV, NQ, MAT><<<grid_for(nc), 256, 0, s>>>(P.M, P.F, P.tab, bc, rec, mask);
     LAUNCH_CHECK();
+    if constexpr (NODE_BITS) {
+      if (node_bits && P.M.nnodes > 0) {
+        k_rec_bcbits<GD, NN, R::SIZE><<<grid_for(P.M.nnodes), 256, 0, s>>>(P.adj_ptr, P.adj_idx, bc, P.M.nnodes, rec, mask);
+        LAUNCH_CHECK();
+      }
+    }
   }
   P.rec = rec;
   P.bcmask = mask;
@@ -5709,6 +5760,10 @@ static int gather_stage(const fa_mesh* mesh, const fa_form* form, const fa_adjac
     HIP_TRY(hipMemset(derr, 0, sizeof(int)));
   }
   P.err = derr;
+  if (adj && adj->ptr && adj->idx) {  // (the prepare stage: the records' bc bits from the nodes, k_rec_bcbits)
+    P.adj_ptr = adj->ptr;
+    P.adj_idx = adj->idx;
+  }
   if (W.mode == GatherStage::ROWS) {
     if (!A || !A->indptr || !A->indices || !A->data) return fail(FA_E_ARG, "null matrix");
     if (A->bs != mesh->gdim || A->nrows != mesh->nnodes) return fail(FA_E_ARG, "matrix shape does not match mesh");

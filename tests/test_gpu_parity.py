@@ -126,6 +126,25 @@ def test_assemble_with_dirichlet(oracle, dev, ct, p, n, method):
     assert np.abs(Ad[rows][:, ~rows]).max(initial=0) == 0.0
 
 
+@pytest.mark.parametrize("ct,p,n", [(-4, 2, (5, 4, 3)), (-4, 1, (6, 5, 4)), (4, 2, (7, 5)), (3, 2, (6, 5)),
+                                    (8, 1, (4, 3, 3))])
+def test_component_dirichlet(oracle, dev, ct, p, n):
+    """Single-component constraints (x = 0: u_x only; y = 0: u_y only, overlapping at the corner):
+    the records' per-dof bc bits (formed from the constrained dofs' side since round 6,
+    k_rec_bcbits) zero exactly those rows / columns."""
+    from femasm import fem
+
+    m, V, a = _setup(oracle, ct, p, n, dev)
+    x0 = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[0], torch.zeros_like(x[0])))
+    y0 = fem.locate_dofs_geometrical(V, lambda x: torch.isclose(x[1], torch.zeros_like(x[1])))
+    bcs = [fem.dirichletbc(0.0, x0, V, components=[0]), fem.dirichletbc(0.0, y0, V, components=[1])]
+    A = fem.assemble_matrix(a, bcs=bcs)
+    marker, _ = fem._combine_bcs(V, bcs)
+    assert 0 < int(marker.sum()) < 2 * V.num_nodes
+    _, _, ref = _oracle_matrix(oracle, V, a, marker=marker, diag=1.0)
+    _assert_close(A, ref)
+
+
 @pytest.mark.parametrize("ct,p,n", [(4, 1, (4, 3)), (4, 2, (3, 3)), (8, 1, (2, 2, 2)), (8, 2, (2, 2, 1))])
 @pytest.mark.parametrize("method", ["gather", "scatter"])
 def test_non_affine_cells(oracle, dev, ct, p, n, method):
