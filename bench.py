@@ -140,7 +140,7 @@ def kernel_hash() -> str:
 
 def measured_traffic(config: str, n: int, world: int):
     """HBM bytes per assembly launch from the committed rocprofv3 PMC record of the same workload
-    (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE, k_cell_records + k_gather), or None.
+    (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE, k_cell_records + k_rec_bcbits + k_gather + k_bc_diag), or None.
     A record of another build of femasm.hip (kernel_hash mismatch) is refused, never reused."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if world != 1 or not os.path.exists(path):
@@ -731,7 +731,7 @@ def main():
                          "traffic_frac": None if traffic_gbps is None else rnd(fracs["traffic_frac"]),
                          "traffic_source": tsrc,
                          "mfma_busy": None if trec is None else trec.get("mfma_busy"),
-                         "kernel": "the assembly launch: per-cell records (or the MFMA element kernel of non-affine "
+                         "kernel": "the assembly launch: per-cell records and their bc bits (or the MFMA element kernel of non-affine "
                                    "hexahedra) + the row gather + the bc diagonal",
                          "launch_ms": round(launch_ms, 4),
                          "algorithmic_bytes": comp["total"],

@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 for cs in ${CFGS:-E:203}; do
   c=${cs%%:*}; n=${cs#*:}
   pm=0; [ "$c" = Dmfma ] && pm=1
-  PASS_MFMA=$pm bash tools/prof_passes.sh gpurun_out/pmc_$c 'k_gather|k_cell_records|k_neo_records|k_hex_mfma|k_bc_diag' -- python bench.py --config $c --side $n --steps 2 --warmup 1 --no-cpu-baseline --no-hbm-probe --no-eneo || exit $?
+  PASS_MFMA=$pm bash tools/prof_passes.sh gpurun_out/pmc_$c 'k_gather|k_cell_records|k_rec_bcbits|k_neo_records|k_hex_mfma|k_bc_diag' -- python bench.py --config $c --side $n --steps 2 --warmup 1 --no-cpu-baseline --no-hbm-probe --no-eneo || exit $?
   python tools/pmc_summary.py gpurun_out/pmc_$c > gpurun_out/pmc_$c.txt || exit $?
   python tools/pmc_summary.py gpurun_out/pmc_$c $c:$n gpurun_out/traffic.json || exit $?
   find gpurun_out/pmc_$c -name "*kernel_trace.csv" -delete

@@ -28,7 +28,7 @@ for k, d in acc.items():
         print(f"  {c:24s} {mean:16.1f}{extra}  [{len(per)} dispatches]")
 
 
-LAUNCH_KERNELS = ("k_gather", "k_cell_records", "k_neo_records", "k_hex_mfma", "k_bc_diag")  # one assembly launch
+LAUNCH_KERNELS = ("k_gather", "k_cell_records", "k_rec_bcbits", "k_neo_records", "k_hex_mfma", "k_bc_diag")  # one assembly launch
 
 
 def counter_total(name, kernels=LAUNCH_KERNELS):
