@@ -1354,7 +1354,8 @@ __global__ __launch_bounds__(256) void k_bc_diag(BsrView A, int64_t nnodes, cons
   const int64_t d0 = A.row_begin * GD, d1 = A.row_end * GD;
   const int64_t a0 = (int64_t)(((uintptr_t)bc + (uintptr_t)d0) & ~(uintptr_t)15) - (int64_t)(uintptr_t)bc;
   // (one search per node instead of per dof, the node queued by its first constrained dof, measured
-  // 0.32 vs 0.26 ms on config E: the first-dof test's byte loads in the scan cost more than it saved)
+  // 0.32 vs 0.26 ms on config E: the first-dof test's byte loads in the scan cost more than it saved;
+  // round 6: the marker bytes taken from the loaded words instead of loaded again, 0.30 vs 0.26 ms)
   auto resolve = [&](int64_t n) {
     const int64_t r = n / GD;
     const int i = (int)(n % GD);
@@ -1681,38 +1682,48 @@ __global__ __launch_bounds__(256) void k_cell_records_staged(MeshView M, FormVie
 // The constrained-dof bits of the uniform-nu records from the constrained nodes' side (round 6): the
 // records kernel then reads no dofmap (40 B per P2 tet of its ~98) and this kernel ORs each constrained
 // node's bits into the records (and the mask array) of the cells around it through the node -> cell
-// adjacency. A wave reads the markers of 64 consecutive nodes (lane = node), then takes its constrained
-// nodes one after the other with a lane per adjacency entry, so an atomic's latency is paid once per
-// constrained node, not once per (node, cell) pair (a thread walking its node's ~24 cells alone: 0.37 ms
-// on config E; per 16 marker bytes and component: 0.66 ms). The same bits as cell_bcmask: bit b * GD + j
-// of cell c for its local node b, component j.
+// adjacency. A wave reads the markers of 8 x 64 consecutive nodes (lane = node, the 8 loads in flight
+// together), then takes its constrained nodes one after the other with a lane per adjacency entry, so an
+// atomic's latency is paid once per constrained node, not once per (node, cell) pair (a thread walking its
+// node's ~24 cells alone: 0.37 ms on config E; per 16 marker bytes and component: 0.66 ms; a wave per 64
+// nodes: 0.26 ms, one load latency per wave). The same bits as cell_bcmask: bit b * GD + j of cell c for
+// its local node b, component j.
 template <int GD, int NN, int RS>
 __global__ __launch_bounds__(256) void k_rec_bcbits(const int64_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj_idx,
                                                     const int8_t* __restrict__ bc, int64_t nnodes, double* __restrict__ rec,
                                                     uint32_t* __restrict__ bcmask) {
   static_assert(NN * GD <= 32, "bc bits of the record word");
+  constexpr int U = 8;  // 64-node groups per wave pass: their marker loads in flight together
   const int lane = threadIdx.x & 63;
   const int64_t wid = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwv = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t base = wid * 64; base < nnodes; base += nwv * 64) {
-    const int64_t n = base + lane;
-    uint32_t nb = 0u;
-    if (n < nnodes) {
+  for (int64_t base = wid * (64 * U); base < nnodes; base += nwv * (64 * U)) {
+    uint32_t nb[U];
 #pragma unroll
-      for (int j = 0; j < GD; ++j) nb |= (bc[n * GD + j] ? 1u : 0u) << j;
+    for (int u = 0; u < U; ++u) {
+      const int64_t n = base + 64 * u + lane;
+      nb[u] = 0u;
+      if (n < nnodes) {
+#pragma unroll
+        for (int j = 0; j < GD; ++j) nb[u] |= (bc[n * GD + j] ? 1u : 0u) << j;
+      }
     }
-    unsigned long long act = __ballot(nb != 0u);
-    while (act) {  // wave-uniform
-      const int l = __ffsll(act) - 1;
-      act &= act - 1;
-      const uint32_t nbl = (uint32_t)__shfl((int)nb, l);
-      const int64_t e0 = adj_ptr[base + l], e1 = adj_ptr[base + l + 1];
-      for (int64_t e = e0 + lane; e < e1; e += 64) {
-        const int64_t p = adj_idx[e];
-        const int64_t c = p / NN;
-        const uint32_t bits = nbl << ((int)(p % NN) * GD);
-        atomicOr(reinterpret_cast<unsigned long long*>(rec + c * RS + GD * GD), (unsigned long long)bits);
-        if (bcmask) atomicOr(bcmask + c, bits);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      unsigned long long act = __ballot(nb[u] != 0u);
+      while (act) {  // wave-uniform
+        const int l = __ffsll(act) - 1;
+        act &= act - 1;
+        const uint32_t nbl = (uint32_t)__shfl((int)nb[u], l);
+        const int64_t nn = base + 64 * u + l;
+        const int64_t e0 = adj_ptr[nn], e1 = adj_ptr[nn + 1];
+        for (int64_t e = e0 + lane; e < e1; e += 64) {
+          const int64_t p = adj_idx[e];
+          const int64_t c = p / NN;
+          const uint32_t bits = nbl << ((int)(p % NN) * GD);
+          atomicOr(reinterpret_cast<unsigned long long*>(rec + c * RS + GD * GD), (unsigned long long)bits);
+          if (bcmask) atomicOr(bcmask + c, bits);
+        }
       }
     }
   }
@@ -5419,7 +5430,8 @@ static int launch_gather(GatherArgs P, const int8_t* bc, hipStream_t s, const Ga
     LAUNCH_CHECK();
     if constexpr (NODE_BITS) {
       if (node_bits && P.M.nnodes > 0) {
-        k_rec_bcbits<GD, NN, R::SIZE><<<grid_for(P.M.nnodes), 256, 0, s>>>(P.adj_ptr, P.adj_idx, bc, P.M.nnodes, rec, mask);
+        k_rec_bcbits<GD, NN, R::SIZE><<<grid_for((P.M.nnodes + 7) / 8), 256, 0, s>>>(P.adj_ptr, P.adj_idx, bc, P.M.nnodes,
+                                                                                  rec, mask);
         LAUNCH_CHECK();
       }
     }
