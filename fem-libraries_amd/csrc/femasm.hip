@@ -1484,6 +1484,7 @@ struct GatherArgs {
   const int32_t* corder;   // [nchunks] visiting order (fa_plan_locality) or NULL (row order)
   const int64_t* chunk_b;  // [nchunks + 1] indptr[row_start[c]] (k_chunk_desc)
   const int64_t* chunk_a;  // [nchunks + 1] adj_ptr[row_start[c]]
+  const int64_t* chunk_desc;  // the plan's cached k_gather_lin chunk arrays (fa_plan_chunk_desc), or NULL
   int64_t nchunks;
   int32_t plan_maxb;        // largest block count of a chunk of the plan (checked against the kernel's)
   int32_t plan_maxadj;      // largest adjacency count of a chunk of the plan
@@ -4675,6 +4676,7 @@ static int plan_gather(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bs
   plan->eadj = nullptr;
   plan->corder = nullptr;
   plan->contrib = nullptr;
+  plan->chunk_desc = nullptr;
   return FA_OK;
 }
 
@@ -5024,6 +5026,7 @@ extern "C" int fa_plan_locality(const fa_mesh* mesh, const fa_adjacency* adj, in
   int rc = check_mesh(mesh);
   if (rc) return rc;
   if (!adj || !adj->ptr || !adj->idx || !corder || !plan || !plan->row_start) return fail(FA_E_ARG, "null argument");
+  plan->chunk_desc = nullptr;  // built for the previous order
   hipStream_t s = (hipStream_t)stream;
   const int64_t n = plan->nchunks;
   if (n >= (1ll << 31)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks (>= 2^31)", (long long)n);
@@ -5058,6 +5061,32 @@ extern "C" int fa_plan_locality(const fa_mesh* mesh, const fa_adjacency* adj, in
   HIP_TRY(hipFreeAsync(buf, s));
   HIP_TRY(hipStreamSynchronize(s));
   plan->corder = corder;
+  return FA_OK;
+}
+
+// The plan's chunk arrays once (fa_plan_chunk_desc): k_lin_chunk_desc as a launch would run it, into a
+// caller-owned buffer kept with the plan.
+__global__ void k_lin_chunk_desc(const int64_t* __restrict__ row_start, int64_t nchunks, const int64_t* __restrict__ indptr,
+                                 int64_t row_begin, const int64_t* __restrict__ adj_ptr, int64_t nent,
+                                 const int32_t* __restrict__ seq, int64_t* __restrict__ cb, int64_t* __restrict__ ca);
+extern "C" int fa_plan_chunk_desc(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, fa_plan* plan,
+                                  int64_t* buf, void* stream) {
+  int rc = check_mesh(mesh);
+  if (rc) return rc;
+  if (!adj || !adj->ptr || !A || !A->indptr || !plan || !plan->row_start || !buf) return fail(FA_E_ARG, "null argument");
+  if (plan->nchunks >= (1ll << 30)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks (>= 2^30)", (long long)plan->nchunks);
+  int64_t wb = A->row_begin, we = A->row_end;
+  if (we <= wb) { wb = 0; we = mesh->nnodes; }
+  if (wb < 0 || we > mesh->nnodes) return fail(FA_E_ARG, "row window out of range");
+  hipStream_t s = (hipStream_t)stream;
+  plan->chunk_desc = nullptr;
+  if (plan->nchunks > 0) {
+    k_lin_chunk_desc<<<grid_for(plan->nchunks), 256, 0, s>>>(plan->row_start, plan->nchunks, A->indptr, wb, adj->ptr,
+                                                             mesh->ncells * mesh->nn, plan->corder, buf,
+                                                             buf + (plan->nchunks + 1));
+    LAUNCH_CHECK();
+  }
+  plan->chunk_desc = buf;
   return FA_OK;
 }
 
@@ -5153,6 +5182,14 @@ __global__ void k_lin_chunk_desc(const int64_t* __restrict__ row_start, int64_t 
 static int lin_chunk_desc(GatherArgs& P, int64_t** buf, hipStream_t s, const int32_t* seq) {
   int rc;
   if (P.nchunks >= (1ll << 30)) return fail(FA_E_CAPACITY, "gather plan has %lld chunks (>= 2^30)", (long long)P.nchunks);
+  if (P.chunk_desc) {  // the plan's arrays (fa_plan_chunk_desc): only the XCD counters per launch
+    if ((rc = scratch_alloc((void**)buf, 1024, s))) return rc;
+    P.chunk_b = P.chunk_desc;
+    P.chunk_a = P.chunk_desc + (P.nchunks + 1);
+    P.ctr = reinterpret_cast<unsigned long long*>(*buf);
+    HIP_TRY(hipMemsetAsync(P.ctr, 0, 1024, s));
+    return FA_OK;
+  }
   if ((rc = scratch_alloc((void**)buf, sizeof(int64_t) * (3 * (P.nchunks + 1) + 128), s))) return rc;
   P.chunk_b = *buf;
   P.chunk_a = *buf + (P.nchunks + 1);
@@ -5695,9 +5732,9 @@ extern "C" int fa_assemble_matrix(const fa_mesh* mesh, const fa_form* form, cons
   if (!scatter) {
     if (!adj || !adj->ptr || !adj->idx || !plan || !plan->row_start)
       return fail(FA_E_ARG, "FA_GATHER needs the adjacency and a plan (fa_plan_gather)");
-    GatherArgs P;
+    GatherArgs P{};
     P.M = M; P.F = F; P.A = Av;
-    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks; P.corder = plan->corder; P.plan_maxb = plan->max_blocks; P.plan_maxadj = plan->max_adj;
+    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks; P.corder = plan->corder; P.chunk_desc = plan->chunk_desc; P.plan_maxb = plan->max_blocks; P.plan_maxadj = plan->max_adj;
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;
@@ -5785,7 +5822,7 @@ static int gather_stage(const fa_mesh* mesh, const fa_form* form, const fa_adjac
     if (!adj || !adj->ptr || !adj->idx || !plan || !plan->row_start)
       return fail(FA_E_ARG, "fa_gather_rows needs the adjacency and a plan (fa_plan_gather)");
     P.A = BsrView{A->indptr, A->indices, A->data, wb, we};
-    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks; P.corder = plan->corder; P.plan_maxb = plan->max_blocks; P.plan_maxadj = plan->max_adj;
+    P.adj_ptr = adj->ptr; P.adj_idx = adj->idx; P.row_start = plan->row_start; P.nchunks = plan->nchunks; P.corder = plan->corder; P.chunk_desc = plan->chunk_desc; P.plan_maxb = plan->max_blocks; P.plan_maxadj = plan->max_adj;
     P.slots = plan->slots;
     P.slot_order = plan->slots ? plan->slot_order : 0;
     P.eadj = P.slot_order ? plan->eadj : nullptr;

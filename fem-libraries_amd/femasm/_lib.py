@@ -84,6 +84,7 @@ class fa_plan(ctypes.Structure):
         ("eadj", ctypes.c_void_p),
         ("corder", ctypes.c_void_p),
         ("contrib", ctypes.c_void_p),
+        ("chunk_desc", ctypes.c_void_p),
     ]
 
 
@@ -95,6 +96,7 @@ SIGNATURES = {
     "fa_version": (ctypes.c_int, []),
     "fa_element_info": (ctypes.c_int, [I32, I32, I32, P, P]),
     "fa_element_table_info": (ctypes.c_int, [I32, I32, I32, P, P]),
+    "fa_plan_chunk_desc": (ctypes.c_int, [P, P, P, P, P, P]),
     "fa_build_adjacency": (ctypes.c_int, [P, P, P, P]),
     "fa_sparsity_count": (ctypes.c_int, [P, P, P, P, P]),
     "fa_sparsity_fill": (ctypes.c_int, [P, P, P, P, P]),

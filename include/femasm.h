@@ -156,6 +156,10 @@ typedef struct {
   const void* contrib;       /* optional contribution plan (fa_plan_contrib): P1/P2 simplices with
                                 linear elasticity of one Poisson ratio then assemble through the
                                 block-owner gather (no per-contribution LDS atomics) */
+  const int64_t* chunk_desc; /* optional device [3 * (nchunks + 1)] (fa_plan_chunk_desc, round 6): the
+                                store-decoupled gathers' per-chunk arrays in the visiting order, built
+                                once per plan instead of at every launch; NULL = built per launch.
+                                Rebuild (or set NULL) after changing corder or row_start */
 } fa_plan;
 
 const char* fa_last_error(void);
@@ -235,6 +239,16 @@ int fa_plan_check_affine(const fa_mesh* mesh, fa_plan* plan, void* stream);
  * buffer of plan->nchunks int32; on success plan->corder points to it. Any permutation assembles
  * the same matrix (each chunk owns its rows); only the re-reads of the records change. */
 int fa_plan_locality(const fa_mesh* mesh, const fa_adjacency* adj, int32_t* corder, fa_plan* plan, void* stream);
+
+/* The chunk arrays the store-decoupled gathers (linear and neo-Hookean) read — per chunk, in the plan's
+ * visiting order (plan->corder, or row order): its first block relative to A's row window, its first
+ * adjacency entry, and its block and entry counts — into a caller-owned device buffer of
+ * 3 * (plan->nchunks + 1) int64, once per plan (plan time, like the slot map); on success
+ * plan->chunk_desc points to it and launches skip rebuilding them (config E: 0.21 ms per assembly, a
+ * full read of the pattern's row pointer and adjacency pointer arrays). A must be the matrix (row
+ * window) the plan was made for. Call it after fa_plan_locality. */
+int fa_plan_chunk_desc(const fa_mesh* mesh, const fa_adjacency* adj, const fa_bsr* A, fa_plan* plan, int64_t* buf,
+                       void* stream);
 
 /* Block-owner gather (P1/P2 triangles and tetrahedra, linear elasticity with one Poisson ratio).
  * fa_plan_gather_contrib chunks the rows for it (like fa_plan_gather, smaller chunks: at most

@@ -200,3 +200,24 @@ def test_deterministic_high_contrast_p1(oracle, dev, contrast):
     ref = _oracle(oracle, V, a, bcs)
     A = fem.assemble_matrix(a, bcs=bcs, deterministic=True)
     assert_rows_close(A.data.cpu().numpy(), ref, A.indptr.cpu().numpy(), RTOL)
+
+
+@pytest.mark.parametrize("ct,p,n", [(-4, 2, (12, 11, 10)), (4, 2, (41, 37)), (-4, 1, (24, 23, 22))])
+def test_cached_chunk_arrays(oracle, dev, ct, p, n):
+    """The plan's chunk arrays built once (fa_plan_chunk_desc, round 6) give the same bits as arrays
+    rebuilt at the launch (plan.chunk_desc = NULL), in every visiting order."""
+    from femasm import fem
+
+    m, V, a, bcs = _problem(oracle, ct, p, n, dev)
+    A = fem.create_matrix(a)
+    for loc in ("row", "morton", "deal"):
+        plan = fem.gather_plan(V, A, 0, a.kind, deterministic=True, locality=loc)
+        assert plan.chunk_desc, "gather_plan builds the chunk arrays"
+        fem.assemble_matrix(a, bcs=bcs, A=A, deterministic=True, plan={"locality": loc})
+        cached = A.data.clone()
+        keep = plan.chunk_desc
+        plan.chunk_desc = None
+        A.data.fill_(float("nan"))
+        fem.assemble_matrix(a, bcs=bcs, A=A, deterministic=True, plan={"locality": loc})
+        plan.chunk_desc = keep
+        assert torch.equal(A.data, cached), loc
