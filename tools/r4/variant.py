@@ -181,6 +181,9 @@ V = {
     "p1tet_nt128": [('constexpr int FA_P1TET_NT = 256;', 'constexpr int FA_P1TET_NT = 128;')],
     "p1tet_nt128_lds8k": [('constexpr int FA_P1TET_NT = 256;', 'constexpr int FA_P1TET_NT = 128;'), ('constexpr int kLinLdsP1 = 16384;', 'constexpr int kLinLdsP1 = 8192;')],
     "p1tet_lds24k": [('constexpr int kLinLdsP1 = 16384;', 'constexpr int kLinLdsP1 = 24576;')],
+    # (round 6) config E's set_diagonal pass: a smaller constrained-dof queue (LDS) per workgroup
+    "bcq1024": [("constexpr int NT = 256, QCAP = 4096;", "constexpr int NT = 256, QCAP = 1024;")],
+    "bcq512": [("constexpr int NT = 256, QCAP = 4096;", "constexpr int NT = 256, QCAP = 512;")],
     # the source as it is (A/B base of an edited product library)
     "base": [],
     # P1 simplices through the records kernel + k_gather_lin (no fused records)
